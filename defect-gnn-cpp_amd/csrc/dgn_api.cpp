@@ -1,0 +1,672 @@
+// dgn_api.cpp — the extern "C" boundary (include/dgn.h): contexts, workspaces, launch
+// sequencing, per-kernel event timing, host staging and the synthetic batch generator.
+// Nothing here computes results on the CPU: there is no fallback path; without a GPU every
+// compute entry point returns DGN_ERR_NODEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dgn.h"
+#include "dgn_internal.hpp"
+
+using namespace dgn;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t b = std::max<size_t>(want, 256);
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+struct KernelStat {
+    int64_t launches = 0;
+    double total_ms = 0.0;
+    double bytes = 0.0;
+    double flops = 0.0;
+};
+
+struct PendingEvent {
+    std::string name;
+    hipEvent_t start, stop;
+};
+
+struct Scalars {  // device-side scalars, one allocation
+    int64_t total;
+    uint32_t max_candidates;
+    uint32_t error_flag;
+    uint32_t work_counter;
+    uint32_t pad;
+};
+
+}  // namespace
+
+struct dgn_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    // graph workspace
+    DevBuf meta, counts, block_sums, scalars;
+    Scalars* host_scalars = nullptr;  // pinned
+    // count->emit handshake
+    bool have_count = false;
+    const double* cnt_pos = nullptr;
+    int64_t cnt_atoms = -1, cnt_structs = -1;
+    double cnt_rc = 0, cnt_eps = 0;
+    uint64_t cnt_k = 0;
+    uint32_t cnt_max_candidates = 0;
+    int64_t cnt_edges = 0;
+    // betti workspace
+    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch;
+    int betti_slots = 0;
+    // host staging
+    DevBuf h_lat, h_pos, h_spec, h_off;
+    // timing
+    bool timing = false;
+    std::vector<PendingEvent> pending;
+    std::vector<hipEvent_t> free_events;
+    std::map<std::string, KernelStat> stats;
+    std::vector<std::string> order;
+};
+
+namespace {
+
+int fail(dgn_ctx* c, int status, const std::string& msg) {
+    if (c) c->last_error = msg;
+    return status;
+}
+int hip_fail(dgn_ctx* c, hipError_t e, const char* where) {
+    return fail(c, DGN_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(ctx, expr)                                      \
+    do {                                                        \
+        hipError_t e_ = (expr);                                 \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr);  \
+    } while (0)
+
+hipEvent_t get_event(dgn_ctx* c) {
+    if (!c->free_events.empty()) {
+        hipEvent_t e = c->free_events.back();
+        c->free_events.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct TimedLaunch {
+    dgn_ctx* c;
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(dgn_ctx* c_, const char* n, double bytes, double flops) : c(c_), name(n) {
+        if (!c->timing) return;
+        auto it = c->stats.find(name);
+        if (it == c->stats.end()) {
+            c->order.push_back(name);
+            it = c->stats.emplace(name, KernelStat{}).first;
+        }
+        it->second.bytes += bytes;
+        it->second.flops += flops;
+        it->second.launches += 1;
+        a = get_event(c);
+        b = get_event(c);
+        (void)hipEventRecord(a, c->stream);
+    }
+    ~TimedLaunch() {
+        if (!c->timing || !a) return;
+        (void)hipEventRecord(b, c->stream);
+        c->pending.push_back({name, a, b});
+    }
+};
+
+void fold_events(dgn_ctx* c) {
+    for (auto& p : c->pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(p.stop) == hipSuccess && hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess)
+            c->stats[p.name].total_ms += ms;
+        c->free_events.push_back(p.start);
+        c->free_events.push_back(p.stop);
+    }
+    c->pending.clear();
+}
+
+bool batch_ok(const dgn_batch* b) {
+    return b && b->num_structures >= 0 && b->num_atoms >= 0 && b->lattice && b->positions && b->atom_offset &&
+           (b->num_atoms == 0 || b->num_structures > 0);
+}
+
+RbfSpec make_rbf(const dgn_graph_params* p) {
+    RbfSpec r;
+    r.dtype = p->rbf_dtype;
+    r.nbins = dgn_rbf_bins(p->rbf_cutoff, p->rbf_dr);
+    r.dr = p->rbf_dr;
+    // edge_features.cpp:13-16
+    const double sigma = p->rbf_cutoff / 3;
+    r.inv_sigma2 = 1 / std::pow(sigma, 2);
+    r.norm = 1 / (sigma * std::sqrt(2 * M_PI));
+    return r;
+}
+
+// graph counting pass shared by the graph and Betti entry points
+int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, double eps, int64_t* num_edges) {
+    const int64_t A = b->num_atoms, B = b->num_structures;
+    const int64_t nblocks = graph_blocks(A);
+    HIP_TRY(c, c->meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
+    HIP_TRY(c, c->counts.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
+    HIP_TRY(c, c->block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(sc, 0, sizeof(Scalars), c->stream));
+    {
+        TimedLaunch t(c, "prep_structures", (double)B * (72 + 16), 0);
+        HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, B, rc, c->meta.as<StructMeta>()));
+    }
+    GraphLaunch g{c->meta.as<StructMeta>(), b->atom_offset, b->positions, B, A, rc * rc, eps, kmax};
+    {
+        TimedLaunch t(c, "graph_count", (double)A * (24 + 4), 0);
+        HIP_TRY(c, launch_graph_count(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
+                                      &sc->max_candidates));
+    }
+    {
+        TimedLaunch t(c, "block_scan", (double)nblocks * 16, 0);
+        HIP_TRY(c, launch_block_scan(c->stream, c->block_sums.as<int64_t>(), nblocks, &sc->total));
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->host_scalars, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->have_count = true;
+    c->cnt_pos = b->positions;
+    c->cnt_atoms = A;
+    c->cnt_structs = B;
+    c->cnt_rc = rc;
+    c->cnt_eps = eps;
+    c->cnt_k = kmax;
+    c->cnt_max_candidates = c->host_scalars->max_candidates;
+    c->cnt_edges = c->host_scalars->total;
+    if (num_edges) *num_edges = c->cnt_edges;
+    return DGN_OK;
+}
+
+int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int32_t* col, double* dist,
+                    double* disp, void* rbf, const RbfSpec& rs) {
+    if (!c->have_count || c->cnt_pos != b->positions || c->cnt_atoms != b->num_atoms)
+        return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
+    const int cap = graph_emit_cap(c->cnt_max_candidates);
+    if (cap == 0)
+        return fail(c, DGN_ERR_UNSUPPORTED, "more than 512 neighbour candidates for one atom (cutoff too large)");
+    if (b->num_atoms == 0) return DGN_OK;
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, sizeof(uint32_t), c->stream));
+    GraphLaunch g{c->meta.as<StructMeta>(), b->atom_offset, b->positions, c->cnt_structs, c->cnt_atoms,
+                  c->cnt_rc * c->cnt_rc, c->cnt_eps, c->cnt_k};
+    const double E = (double)c->cnt_edges, A = (double)c->cnt_atoms;
+    const double rbf_bytes = rs.dtype == DGN_F32 ? 4.0 : (rs.dtype == DGN_F64 ? 8.0 : 0.0);
+    const double bytes = A * 24 + (double)c->cnt_structs * 72 + 8 * (A + 1) + 4 * A + E * (4 + (dist ? 8 : 0)) +
+                         (disp ? 24 * E : 0) + (rbf ? E * rs.nbins * rbf_bytes : 0);
+    {
+        TimedLaunch t(c, "graph_emit", bytes, 0);
+        HIP_TRY(c, launch_graph_emit(c->stream, g, cap, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
+                                     const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs, &sc->error_flag));
+    }
+    return DGN_OK;
+}
+
+int check_emit_flag(dgn_ctx* c) {
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->host_scalars->error_flag)
+        return fail(c, DGN_ERR_INTERNAL, "graph emit consistency flag " + std::to_string(c->host_scalars->error_flag));
+    return DGN_OK;
+}
+
+int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int32_t* counts, const double* clouds,
+               const int32_t* npoints, int32_t cloud_stride, int64_t num_clouds, float* pairs_out, int32_t pair_cap) {
+    const int64_t A = clouds ? num_clouds : b->num_atoms;
+    if (A == 0) return DGN_OK;
+    int max_points = cloud_stride;
+    if (!clouds) {
+        int64_t E = 0;
+        int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E);
+        if (st) return st;
+        HIP_TRY(c, c->b_row_ptr.ensure(sizeof(int64_t) * (size_t)(A + 1)));
+        HIP_TRY(c, c->b_col.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(E, 1)));
+        HIP_TRY(c, c->b_dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(E, 1)));
+        HIP_TRY(c, c->b_disp.ensure(sizeof(double) * 3 * (size_t)std::max<int64_t>(E, 1)));
+        RbfSpec none{};
+        none.dtype = DGN_NONE;
+        st = graph_emit_impl(c, b, c->b_row_ptr.as<int64_t>(), c->b_col.as<int32_t>(), c->b_dist.as<double>(),
+                             c->b_disp.as<double>(), nullptr, none);
+        if (st) return st;
+        max_points = (int)c->cnt_max_candidates + 1;
+    }
+    if (max_points > betti_max_points())
+        return fail(c, DGN_ERR_UNSUPPORTED,
+                    "local complex with " + std::to_string(max_points) + " points exceeds the " +
+                        std::to_string(betti_max_points()) + "-point wave64 kernel envelope (see DESIGN.md)");
+    if (c->betti_slots == 0) c->betti_slots = betti_grid_waves(c->device);
+    const int64_t spw = betti_scratch_bytes_per_wave();
+    HIP_TRY(c, c->b_scratch.ensure((size_t)spw * c->betti_slots));
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
+    sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 2 * sizeof(uint32_t), c->stream));
+    BettiLaunch bl{};
+    bl.row_ptr = clouds ? nullptr : c->b_row_ptr.as<int64_t>();
+    bl.disp = clouds ? nullptr : c->b_disp.as<double>();
+    bl.pos = clouds ? nullptr : b->positions;
+    bl.species = clouds ? nullptr : b->species;
+    bl.atom_offset = clouds ? nullptr : b->atom_offset;
+    bl.num_structures = clouds ? 0 : b->num_structures;
+    bl.num_atoms = A;
+    bl.thr = (float)rc;  // ripser_wrapper.cpp:28
+    bl.features = features;
+    bl.counts = counts;
+    bl.error_flag = &sc->error_flag;
+    bl.work_counter = &sc->work_counter;
+    bl.scratch = c->b_scratch.as<uint8_t>();
+    bl.scratch_per_wave = spw;
+    bl.clouds = clouds;
+    bl.npoints = npoints;
+    bl.cloud_stride = cloud_stride;
+    bl.pairs_out = pairs_out;
+    bl.pair_cap = pair_cap;
+    {
+        // algorithmic bytes: CSR rows in (disp 24 B/edge + row_ptr) + positions + 35 f64 + 4 i32 out;
+        // flops: 6 n^2 per complex for the Gram product is accounted in DESIGN.md, not here
+        const double bytes = clouds ? 0.0 : ((double)c->cnt_edges * 24 + (double)A * (8 + 24 + 4 + 35 * 8 + 16));
+        TimedLaunch t(c, "betti_vr", bytes, 0);
+        HIP_TRY(c, launch_betti(c->stream, bl, max_points, c->betti_slots));
+    }
+    HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint32_t f = c->host_scalars->error_flag;
+    if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
+    if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
+    if (f) return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
+    return DGN_OK;
+}
+
+// stage a host batch into context-owned device buffers
+int stage_batch(dgn_ctx* c, const dgn_batch* h, dgn_batch* d) {
+    if (!batch_ok(h)) return fail(c, DGN_ERR_ARG, "invalid batch");
+    const int64_t A = h->num_atoms, B = h->num_structures;
+    HIP_TRY(c, c->h_lat.ensure(sizeof(double) * 9 * (size_t)std::max<int64_t>(B, 1)));
+    HIP_TRY(c, c->h_pos.ensure(sizeof(double) * 3 * (size_t)std::max<int64_t>(A, 1)));
+    HIP_TRY(c, c->h_spec.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
+    HIP_TRY(c, c->h_off.ensure(sizeof(int64_t) * (size_t)(B + 1)));
+    HIP_TRY(c, hipMemcpyAsync(c->h_lat.p, h->lattice, sizeof(double) * 9 * B, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_pos.p, h->positions, sizeof(double) * 3 * A, hipMemcpyHostToDevice, c->stream));
+    if (h->species)
+        HIP_TRY(c, hipMemcpyAsync(c->h_spec.p, h->species, sizeof(int32_t) * A, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_off.p, h->atom_offset, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, c->stream));
+    *d = *h;
+    d->lattice = c->h_lat.as<double>();
+    d->positions = c->h_pos.as<double>();
+    d->species = h->species ? c->h_spec.as<int32_t>() : nullptr;
+    d->atom_offset = c->h_off.as<int64_t>();
+    return DGN_OK;
+}
+
+// splitmix64 (see defect-gnn-cpp_amd/python/dgn/synth.py for the contract)
+inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+}  // namespace
+
+// ======================================= C ABI ============================================
+extern "C" {
+
+const char* dgn_status_string(int s) {
+    switch (s) {
+        case DGN_OK: return "ok";
+        case DGN_ERR_ARG: return "invalid argument";
+        case DGN_ERR_HIP: return "HIP runtime error";
+        case DGN_ERR_CAPACITY: return "capacity exceeded";
+        case DGN_ERR_NODEVICE: return "no GPU device (there is no CPU fallback)";
+        case DGN_ERR_UNSUPPORTED: return "outside the implemented envelope";
+        case DGN_ERR_INTERNAL: return "internal consistency check failed";
+        default: return "unknown status";
+    }
+}
+
+int dgn_ctx_create(int device, dgn_ctx** out) {
+    if (!out) return DGN_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DGN_ERR_NODEVICE;
+    if (device < 0 || device >= n) return DGN_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return DGN_ERR_HIP;
+    dgn_ctx* c = new dgn_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return DGN_ERR_HIP;
+    }
+    c->stream = c->own;
+    if (hipHostMalloc((void**)&c->host_scalars, sizeof(Scalars), hipHostMallocDefault) != hipSuccess) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return DGN_ERR_HIP;
+    }
+    *out = c;
+    return DGN_OK;
+}
+
+void dgn_ctx_destroy(dgn_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    fold_events(c);
+    for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
+    for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
+                      &c->b_disp, &c->b_scratch, &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
+        b->release();
+    if (c->host_scalars) (void)hipHostFree(c->host_scalars);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
+    if (!c) return DGN_ERR_ARG;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+    return DGN_OK;
+}
+
+int dgn_ctx_synchronize(dgn_ctx* c) {
+    if (!c) return DGN_ERR_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return DGN_OK;
+}
+
+const char* dgn_ctx_last_error(const dgn_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
+
+int dgn_ctx_enable_timing(dgn_ctx* c, int on) {
+    if (!c) return DGN_ERR_ARG;
+    c->timing = on != 0;
+    return DGN_OK;
+}
+
+int dgn_ctx_reset_timing(dgn_ctx* c) {
+    if (!c) return DGN_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    fold_events(c);
+    c->stats.clear();
+    c->order.clear();
+    return DGN_OK;
+}
+
+int dgn_ctx_kernel_times(dgn_ctx* c, dgn_kernel_time* out, int cap) {
+    if (!c) return -DGN_ERR_ARG;
+    (void)hipStreamSynchronize(c->stream);
+    fold_events(c);
+    int k = 0;
+    for (const std::string& name : c->order) {
+        if (out && k < cap) {
+            const KernelStat& s = c->stats[name];
+            std::memset(&out[k], 0, sizeof(dgn_kernel_time));
+            std::snprintf(out[k].name, sizeof(out[k].name), "%s", name.c_str());
+            out[k].launches = s.launches;
+            out[k].total_ms = s.total_ms;
+            out[k].bytes = s.bytes;
+            out[k].flops = s.flops;
+        }
+        ++k;
+    }
+    return k;
+}
+
+void dgn_graph_params_default(dgn_graph_params* p) {
+    if (!p) return;
+    // include/graph/neighbor_list.hpp:19-22 and include/graph/crystal_graph.hpp:14-19
+    p->r_cutoff = 10.0;
+    p->max_neighbors = 20;
+    p->epsilon = 1e-10;
+    p->rbf_cutoff = 10.0;
+    p->rbf_dr = 0.1;
+    p->rbf_dtype = DGN_F32;
+    p->write_displacement = 0;
+}
+
+int dgn_rbf_bins(double rc, double dr) { return (int)std::floor(rc / dr); }  // edge_features.cpp:13
+
+int dgn_dev_graph_count(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* p, int64_t* num_edges) {
+    if (!c || !p || !batch_ok(b) || !(p->r_cutoff > 0)) return fail(c, DGN_ERR_ARG, "dgn_dev_graph_count: bad args");
+    HIP_TRY(c, hipSetDevice(c->device));
+    return graph_count_impl(c, b, p->r_cutoff, p->max_neighbors, p->epsilon, num_edges);
+}
+
+int dgn_dev_graph_emit(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* p, int64_t* row_ptr,
+                       const dgn_graph_out* o) {
+    if (!c || !p || !batch_ok(b) || !o || !row_ptr || !o->col_idx) return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: bad args");
+    if (p->r_cutoff != c->cnt_rc || p->max_neighbors != c->cnt_k || p->epsilon != c->cnt_eps)
+        return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: parameters differ from the count pass");
+    if (p->rbf_dtype != DGN_NONE && (!(p->rbf_dr > 0) || dgn_rbf_bins(p->rbf_cutoff, p->rbf_dr) <= 0))
+        return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: bad RBF parameters");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const RbfSpec rs = make_rbf(p);
+    return graph_emit_impl(c, b, row_ptr, o->col_idx, o->distance, p->write_displacement ? o->displacement : nullptr,
+                           p->rbf_dtype != DGN_NONE ? o->rbf : nullptr, rs);
+}
+
+int dgn_host_graph(dgn_ctx* c, const dgn_batch* h, const dgn_graph_params* p, dgn_graph_result** out) {
+    if (!c || !p || !out) return fail(c, DGN_ERR_ARG, "dgn_host_graph: bad args");
+    *out = nullptr;
+    HIP_TRY(c, hipSetDevice(c->device));
+    dgn_batch d;
+    int st = stage_batch(c, h, &d);
+    if (st) return st;
+    int64_t E = 0;
+    if ((st = dgn_dev_graph_count(c, &d, p, &E))) return st;
+    const int nb = p->rbf_dtype != DGN_NONE ? dgn_rbf_bins(p->rbf_cutoff, p->rbf_dr) : 0;
+    const size_t rbf_elem = p->rbf_dtype == DGN_F64 ? 8 : 4;
+    const int64_t A = h->num_atoms;
+    DevBuf rp, col, dist, disp, rbf;
+    auto cleanup = [&]() {
+        rp.release();
+        col.release();
+        dist.release();
+        disp.release();
+        rbf.release();
+    };
+    hipError_t e;
+    if ((e = rp.ensure(8 * (A + 1))) || (e = col.ensure(4 * std::max<int64_t>(E, 1))) ||
+        (e = dist.ensure(8 * std::max<int64_t>(E, 1))) ||
+        (p->write_displacement && (e = disp.ensure(24 * std::max<int64_t>(E, 1)))) ||
+        (nb && (e = rbf.ensure(rbf_elem * nb * std::max<int64_t>(E, 1))))) {
+        cleanup();
+        return hip_fail(c, e, "dgn_host_graph: device allocation");
+    }
+    if (A == 0) HIP_TRY(c, hipMemsetAsync(rp.p, 0, 8, c->stream));
+    dgn_graph_out o{col.as<int32_t>(), dist.as<double>(), disp.as<double>(), rbf.p};
+    if ((st = dgn_dev_graph_emit(c, &d, p, rp.as<int64_t>(), &o)) || (st = check_emit_flag(c))) {
+        cleanup();
+        return st;
+    }
+    dgn_graph_result* r = new dgn_graph_result();
+    std::memset(r, 0, sizeof(*r));
+    r->num_atoms = A;
+    r->num_edges = E;
+    r->n_rbf = nb;
+    r->rbf_dtype = nb ? p->rbf_dtype : DGN_NONE;
+    r->row_ptr = new int64_t[A + 1];
+    r->col_idx = new int32_t[std::max<int64_t>(E, 1)];
+    r->distance = new double[std::max<int64_t>(E, 1)];
+    if (p->write_displacement) r->displacement = new double[3 * std::max<int64_t>(E, 1)];
+    if (nb) r->rbf = ::operator new(rbf_elem * nb * std::max<int64_t>(E, 1));
+    e = hipMemcpy(r->row_ptr, rp.p, 8 * (A + 1), hipMemcpyDeviceToHost);
+    if (!e && E) e = hipMemcpy(r->col_idx, col.p, 4 * E, hipMemcpyDeviceToHost);
+    if (!e && E) e = hipMemcpy(r->distance, dist.p, 8 * E, hipMemcpyDeviceToHost);
+    if (!e && E && r->displacement) e = hipMemcpy(r->displacement, disp.p, 24 * E, hipMemcpyDeviceToHost);
+    if (!e && E && r->rbf) e = hipMemcpy(r->rbf, rbf.p, rbf_elem * nb * E, hipMemcpyDeviceToHost);
+    cleanup();
+    if (e) {
+        dgn_graph_result_free(r);
+        return hip_fail(c, e, "dgn_host_graph: copy back");
+    }
+    *out = r;
+    return DGN_OK;
+}
+
+void dgn_graph_result_free(dgn_graph_result* r) {
+    if (!r) return;
+    delete[] r->row_ptr;
+    delete[] r->col_idx;
+    delete[] r->distance;
+    delete[] r->displacement;
+    ::operator delete(r->rbf);
+    delete r;
+}
+
+int dgn_dev_betti(dgn_ctx* c, const dgn_batch* b, const dgn_betti_params* p, double* features, int32_t* counts) {
+    if (!c || !p || !batch_ok(b) || !b->species || !features || !(p->r_cutoff > 0))
+        return fail(c, DGN_ERR_ARG, "dgn_dev_betti: bad args");
+    HIP_TRY(c, hipSetDevice(c->device));
+    return betti_impl(c, b, p->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0);
+}
+
+int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, double* features, int32_t* counts) {
+    if (!c || !p || !features || !h || !h->species) return fail(c, DGN_ERR_ARG, "dgn_host_betti: bad args");
+    HIP_TRY(c, hipSetDevice(c->device));
+    dgn_batch d;
+    int st = stage_batch(c, h, &d);
+    if (st) return st;
+    const int64_t A = h->num_atoms;
+    DevBuf f, k;
+    hipError_t e;
+    if ((e = f.ensure(8 * 35 * std::max<int64_t>(A, 1))) || (e = k.ensure(16 * std::max<int64_t>(A, 1))))
+        return hip_fail(c, e, "dgn_host_betti: allocation");
+    st = dgn_dev_betti(c, &d, p, f.as<double>(), k.as<int32_t>());
+    if (st == DGN_OK || st == DGN_ERR_CAPACITY || st == DGN_ERR_UNSUPPORTED) {
+        if (A) {
+            e = hipMemcpy(features, f.p, 8 * 35 * A, hipMemcpyDeviceToHost);
+            if (!e && counts) e = hipMemcpy(counts, k.p, 16 * A, hipMemcpyDeviceToHost);
+            if (e) st = hip_fail(c, e, "dgn_host_betti: copy back");
+        }
+    }
+    f.release();
+    k.release();
+    return st;
+}
+
+int dgn_host_persistence(dgn_ctx* c, const double* clouds, const int32_t* npoints, int64_t C, int32_t max_points,
+                         double threshold, float* pairs, int32_t cap, int32_t* counts) {
+    if (!c || !clouds || !npoints || C < 0 || max_points <= 0 || cap <= 0)
+        return fail(c, DGN_ERR_ARG, "dgn_host_persistence: bad args");
+    if (C == 0) return DGN_OK;
+    for (int64_t i = 0; i < C; ++i)
+        if (npoints[i] < 1 || npoints[i] > max_points) return fail(c, DGN_ERR_ARG, "npoints out of range");
+    HIP_TRY(c, hipSetDevice(c->device));
+    DevBuf dc, dn, dp, dk;
+    hipError_t e;
+    if ((e = dc.ensure(24 * (size_t)C * max_points)) || (e = dn.ensure(4 * (size_t)C)) ||
+        (e = dp.ensure(8 * 3 * (size_t)C * cap)) || (e = dk.ensure(16 * (size_t)C)))
+        return hip_fail(c, e, "dgn_host_persistence: allocation");
+    HIP_TRY(c, hipMemcpy(dc.p, clouds, 24 * (size_t)C * max_points, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(dn.p, npoints, 4 * (size_t)C, hipMemcpyHostToDevice));
+    int st = betti_impl(c, nullptr, threshold, nullptr, dk.as<int32_t>(), dc.as<double>(), dn.as<int32_t>(), max_points,
+                        C, dp.as<float>(), cap);
+    std::vector<int32_t> kk(4 * C);
+    if (!st) {
+        HIP_TRY(c, hipMemcpy(kk.data(), dk.p, 16 * (size_t)C, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(pairs, dp.p, 8 * 3 * (size_t)C * cap, hipMemcpyDeviceToHost));
+        // sort each diagram ascending by (birth, death) for a canonical order
+        for (int64_t i = 0; i < C; ++i) {
+            const int n_per[3] = {kk[4 * i], kk[4 * i + 2], kk[4 * i + 3]};
+            for (int d = 0; d < 3; ++d) {
+                std::pair<float, float>* P = reinterpret_cast<std::pair<float, float>*>(pairs + ((i * 3 + d) * cap) * 2);
+                std::sort(P, P + std::min(n_per[d], cap));
+            }
+        }
+        if (counts) std::memcpy(counts, kk.data(), 16 * (size_t)C);
+        for (int64_t i = 0; i < C; ++i)
+            if (kk[4 * i] > cap || kk[4 * i + 2] > cap || kk[4 * i + 3] > cap) st = fail(c, DGN_ERR_CAPACITY, "pair cap");
+    }
+    dc.release();
+    dn.release();
+    dp.release();
+    dk.release();
+    return st;
+}
+
+int64_t dgn_synth_atoms_per_structure(int kind, int m) {
+    if (m <= 0) return -1;
+    return kind == 0 ? (int64_t)m * m * m : kind == 1 ? 4LL * m * m * m : -1;
+}
+
+int dgn_synth_batch(int kind, int m, int64_t B, int64_t first_id, double* lattice, double* positions, int32_t* species,
+                    int64_t* atom_offset) {
+    const int64_t n = dgn_synth_atoms_per_structure(kind, m);
+    if (n <= 0 || B < 0 || !lattice || !positions || !atom_offset) return DGN_ERR_ARG;
+    const double s = kind == 0 ? 2.32 : std::pow(4.0 / 0.08, 1.0 / 3.0);
+    const double L = m * s;
+    static const double basis[4][3] = {{0, 0, 0}, {0.5, 0.5, 0}, {0.5, 0, 0.5}, {0, 0.5, 0.5}};
+    for (int64_t b = 0; b < B; ++b) {
+        double* lat = lattice + 9 * b;
+        for (int k = 0; k < 9; ++k) lat[k] = 0.0;
+        lat[0] = lat[4] = lat[8] = L;
+        atom_offset[b] = b * n;
+        const uint64_t seed = 0x5EED0000ull + (uint64_t)(first_id + b);
+        uint64_t draw = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            double base[3];
+            int sp;
+            if (kind == 0) {
+                const int64_t ix = i / ((int64_t)m * m), iy = (i / m) % m, iz = i % m;
+                base[0] = (double)ix + 0.5;
+                base[1] = (double)iy + 0.5;
+                base[2] = (double)iz + 0.5;
+                sp = (int)((ix + iy + iz) % 2);
+            } else {
+                const int64_t cell = i / 4, bb = i % 4;
+                const int64_t cx = cell / ((int64_t)m * m), cy = (cell / m) % m, cz = cell % m;
+                base[0] = ((double)cx + basis[bb][0]) + 0.25;
+                base[1] = ((double)cy + basis[bb][1]) + 0.25;
+                base[2] = ((double)cz + basis[bb][2]) + 0.25;
+                sp = (int)(bb % 2);
+            }
+            double* p = positions + 3 * (b * n + i);
+            for (int k = 0; k < 3; ++k) {
+                ++draw;
+                const uint64_t z = mix64(seed + draw * 0x9E3779B97F4A7C15ull);
+                const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+                p[k] = base[k] * s + (0.1 * u - 0.05) * s;
+            }
+            if (species) species[b * n + i] = sp;
+        }
+    }
+    atom_offset[B] = B * n;
+    return DGN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// dgn_internal.hpp — host-side launchers shared between the C ABI (dgn_api.cpp) and the
+// kernel translation units. Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dgn_device.hpp"
+
+namespace dgn {
+
+constexpr int kGraphBlock = 256;          // 4 waves
+constexpr int kAtomsPerBlock = 16;        // 4 query atoms per wave, processed in turn
+constexpr int kScanThreads = 1024;
+
+struct GraphLaunch {
+    const StructMeta* meta;
+    const int64_t* atom_offset;
+    const double* pos;
+    int64_t num_structures, num_atoms;
+    double rc2, eps;
+    uint64_t kmax;
+};
+
+struct RbfSpec {
+    int32_t dtype;  // DGN_NONE / DGN_F32 / DGN_F64
+    int32_t nbins;
+    double dr, inv_sigma2, norm;
+};
+
+hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset,
+                                  int64_t num_structures, double rc, StructMeta* meta);
+hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
+                              uint32_t* max_candidates);
+hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, int64_t nblocks, int64_t* total);
+// cap: candidate capacity per query atom (>= max candidates from the count pass)
+hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const int32_t* counts,
+                             const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
+                             double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag);
+
+inline int64_t graph_blocks(int64_t num_atoms) { return (num_atoms + kAtomsPerBlock - 1) / kAtomsPerBlock; }
+int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
+
+// ---- Betti ----
+struct BettiLaunch {
+    const int64_t* row_ptr;   // CSR from the graph emit (K = unlimited), sorted by distance
+    const double* disp;       // [E][3]
+    const double* pos;        // [A][3]
+    const int32_t* species;   // [A]
+    const int64_t* atom_offset;
+    int64_t num_structures, num_atoms;
+    float thr;                // (float) r_cutoff
+    double* features;         // [A][35]
+    int32_t* counts;          // [A][4] or null
+    uint32_t* error_flag;
+    uint32_t* work_counter;   // persistent work queue
+    uint8_t* scratch;         // per-wave global scratch
+    int64_t scratch_per_wave;
+    // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
+    const double* clouds;
+    const int32_t* npoints;
+    int32_t cloud_stride;     // max_points
+    // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
+    float* pairs_out;
+    int32_t pair_cap;
+};
+int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
+int64_t betti_scratch_bytes_per_wave();
+int betti_grid_waves(int device);
+hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int grid_waves);
+
+}  // namespace dgn

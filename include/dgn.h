@@ -1,0 +1,165 @@
+/*
+ * dgn.h — C ABI of the MI355X-native crystal-graph + Betti feature path (libdgn.so).
+ *
+ * Drop-in boundary for the reference's include/graph and include/topology hot path
+ * (bamarler/Defect-GNN-cpp). Plain pointers and sizes only; no exceptions cross this
+ * boundary; every entry point returns a dgn_status. Each function names the reference
+ * interface it replaces (file:line in the reference tree).
+ *
+ * Two levels:
+ *   dgn_dev_*  : device pointers (HBM-resident inputs/outputs), asynchronous on the context's
+ *                stream except where noted. This is what the bench times.
+ *   dgn_host_* : host pointers; the library stages through its own device buffers. This is
+ *                what the C++ facade (defect-gnn-cpp_amd/cpp) and FFI callers use.
+ *
+ * Threading: one context per device/stream; calls on different contexts are thread-safe;
+ * a context must not be used from two threads at once (reference: NeighborList is immutable
+ * after construction, include/graph/neighbor_list.hpp:19-24; Ripser spawns its own threads —
+ * num_threads is accepted and ignored on this path).
+ */
+#ifndef DGN_H
+#define DGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------------------- */
+typedef enum {
+    DGN_OK = 0,
+    DGN_ERR_ARG = 1,         /* bad argument (reference: std::out_of_range / UB)            */
+    DGN_ERR_HIP = 2,         /* HIP runtime error                                         */
+    DGN_ERR_CAPACITY = 3,    /* caller buffer too small / per-complex workspace overflow  */
+    DGN_ERR_NODEVICE = 4,    /* no GPU visible — there is NO CPU fallback                  */
+    DGN_ERR_UNSUPPORTED = 5, /* outside the implemented envelope           */
+    DGN_ERR_INTERNAL = 6     /* a device-side consistency check failed                    */
+} dgn_status;
+
+const char* dgn_status_string(int status);
+
+/* ---- context -------------------------------------------------------------------------- */
+typedef struct dgn_ctx dgn_ctx;
+
+int dgn_ctx_create(int device, dgn_ctx** out);
+void dgn_ctx_destroy(dgn_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL = the context's own. */
+int dgn_ctx_set_stream(dgn_ctx* ctx, void* hip_stream);
+int dgn_ctx_synchronize(dgn_ctx* ctx);
+const char* dgn_ctx_last_error(const dgn_ctx* ctx);
+
+/* Per-kernel timing with hipEvents recorded on the launch stream around every launch. */
+typedef struct {
+    char name[48];
+    int64_t launches;
+    double total_ms;
+    /* algorithmic bytes / flops the launches were accounted for */
+    double bytes;
+    double flops;
+} dgn_kernel_time;
+int dgn_ctx_enable_timing(dgn_ctx* ctx, int on);
+/* Synchronizes, folds pending events, returns the number of kernel records (<= cap copied). */
+int dgn_ctx_kernel_times(dgn_ctx* ctx, dgn_kernel_time* out, int cap);
+int dgn_ctx_reset_timing(dgn_ctx* ctx);
+
+/* ---- batched input (replaces crystal::Structure, src/crystal/structure.cpp:7-20) -------- */
+typedef struct {
+    int64_t num_structures;
+    int64_t num_atoms;          /* total atoms over all structures                      */
+    const double* lattice;      /* [B][3][3] row-major, rows = a, b, c (Structure::lattice)  */
+    const double* positions;    /* [A][3] Cartesian (Atom::position = L^T * frac)       */
+    const int32_t* species;     /* [A] species index (Atom::element, vasp_parser.cpp:66) */
+    const int64_t* atom_offset; /* [B+1] first atom of each structure                   */
+} dgn_batch;
+
+/* ---- graph: NeighborList + gaussian_rbf + CrystalGraph edge part ----------------------
+ * Replaces graph::NeighborList(structure, r_cutoff=10, max_neighbors=20, epsilon=1e-10)
+ * (include/graph/neighbor_list.hpp:19-22, src/graph/neighbor_list.cpp:14-94), the per-edge
+ * gaussian_rbf(distance, r_cutoff, dr) (src/graph/edge_features.cpp:7-24) and the edge loop of
+ * CrystalGraph (src/graph/crystal_graph.cpp:23-40).
+ * Output CSR: rows = atoms of the whole batch in order; row_ptr is global (int64); col_idx is
+ * the neighbour's index WITHIN its structure (Neighbor::idx); edges of a row are sorted by
+ * (distance, idx, image) and truncated to max_neighbors. */
+enum { DGN_NONE = 0, DGN_F32 = 1, DGN_F64 = 2 };
+
+typedef struct {
+    double r_cutoff;        /* NeighborList r_cutoff (reference default 10.0)           */
+    uint64_t max_neighbors; /* reference default 20; UINT64_MAX = unlimited           */
+    double epsilon;         /* self-image skip threshold (1e-10)                      */
+    double rbf_cutoff;      /* CrystalGraph r_cutoff for the RBF (default 10.0)       */
+    double rbf_dr;          /* CrystalGraph dr (default 0.1)                          */
+    int32_t rbf_dtype;      /* DGN_F32 (default), DGN_F64, DGN_NONE                    */
+    int32_t write_displacement; /* also emit Neighbor::displacement [E][3] f64         */
+} dgn_graph_params;
+
+void dgn_graph_params_default(dgn_graph_params* p);
+int dgn_rbf_bins(double rbf_cutoff, double rbf_dr); /* floor(rc/dr), edge_features.cpp:13 */
+
+typedef struct {
+    int32_t* col_idx;      /* [E]                                                  */
+    double* distance;      /* [E]                                                  */
+    double* displacement;  /* [E][3] or NULL                                        */
+    void* rbf;             /* [E][n_rbf] row-major f32/f64 or NULL                  */
+} dgn_graph_out;
+
+/* Phase 1 (device): per-atom counts and their scan are kept in the context; the total edge
+ * count E is copied to *num_edges (this call synchronizes the stream once). */
+int dgn_dev_graph_count(dgn_ctx* ctx, const dgn_batch* batch, const dgn_graph_params* p,
+                        int64_t* num_edges);
+/* Phase 2 (device, async): write row_ptr[A+1] and fill the CSR + edge features (capacity E from
+ * phase 1). Must follow dgn_dev_graph_count on the same context with the same batch/params. */
+int dgn_dev_graph_emit(dgn_ctx* ctx, const dgn_batch* batch, const dgn_graph_params* p,
+                       int64_t* row_ptr, const dgn_graph_out* out);
+
+/* Host-level convenience: the library owns the result; free with dgn_graph_result_free. */
+typedef struct {
+    int64_t num_atoms, num_edges;
+    int32_t n_rbf, rbf_dtype;
+    int64_t* row_ptr;
+    int32_t* col_idx;
+    double* distance;
+    double* displacement; /* NULL unless requested */
+    void* rbf;            /* NULL if DGN_NONE       */
+} dgn_graph_result;
+int dgn_host_graph(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_graph_params* p,
+                   dgn_graph_result** out);
+void dgn_graph_result_free(dgn_graph_result* r);
+
+/* ---- topology: per-atom 35-d Betti statistics -------------------------------------------
+ * Replaces topology::compute_structure_betti_features(structure, r_cutoff=10, threads=8)
+ * (include/topology/betti_features.hpp:37-39, src/topology/betti_features.cpp:57-119), i.e.
+ * NeighborList(rc, SIZE_MAX) + compute_persistence (src/topology/ripser_wrapper.cpp:11-70,
+ * Ripser dim 2, Z/2, threshold rc) + compute_statistics (betti_features.cpp:24-55).
+ * features: [A][35] f64 row-major (the facade transposes to the reference's column-major
+ * per-structure MatrixXd). counts (optional): [A][4] int32 = #dim0 finite, #dim0 infinite,
+ * #dim1, #dim2 pairs exactly as the reference emits them (death > birth; essential dim>=1
+ * classes are not emitted). An isolated atom yields 35 zeros and counts (0,1,0,0)
+ * (the reference segfaults, third_party/ripser/ripser.cpp:761). */
+typedef struct {
+    double r_cutoff; /* reference default 10.0 */
+} dgn_betti_params;
+
+int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* p, double* features,
+                  int32_t* counts);
+int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
+                   double* features, int32_t* counts);
+
+/* Local-complex persistence from point clouds (replaces topology::compute_persistence,
+ * src/topology/ripser_wrapper.cpp:60-70). clouds: [C][max_points][3] f64 (host), npoints[C].
+ * pairs: [C][3][cap][2] f32 (host) sorted ascending by (birth, death); counts [C][4]. */
+int dgn_host_persistence(dgn_ctx* ctx, const double* clouds, const int32_t* npoints, int64_t num_clouds,
+                         int32_t max_points, double threshold, float* pairs, int32_t cap, int32_t* counts);
+
+/* ---- synthetic batches (bench/test inputs) -----------------------
+ * kind 0 = simple cubic m^3 (s = 2.32 A), kind 1 = FCC m^3 cells (a = 3.684 A). Host arrays:
+ * lattice [B][9], positions [B*n][3], species [B*n], atom_offset [B+1]. */
+int64_t dgn_synth_atoms_per_structure(int kind, int m);
+int dgn_synth_batch(int kind, int m, int64_t num_structures, int64_t first_id, double* lattice,
+                    double* positions, int32_t* species, int64_t* atom_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGN_H */

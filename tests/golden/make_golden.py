@@ -1,0 +1,142 @@
+"""Generate the committed golden fixtures (run ONLY in the survey/build container).
+
+    python tests/golden/make_golden.py
+
+Inputs: the reference's own POSCAR files (/root/reference/web/public/data/structures/*.vasp,
+parsed here as data) and synthetic SC cells from the bit-reproducible generator.
+Expected outputs: the CPU restatement (oracle/liboracle.so) for the neighbour list, RBF and Gram
+distances, and the reference's VERBATIM vendored Ripser (oracle/_ref/libdgn_ref.so, compiled from
+/root/reference/third_party/ripser) for persistence pairs, counts and the 35 statistics. The script
+asserts that the restated reduction agrees with verbatim Ripser on every complex it writes.
+
+Outputs (tests/golden/*.npz, small): no reference source text is stored, only arrays.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "defect-gnn-cpp_amd", "python")]
+import oracle_py as O  # noqa: E402
+from dgn import synth  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+REF_POSCARS = "/root/reference/web/public/data/structures"
+
+
+def parse_poscar(path):
+    """vasp_parser.cpp:13-78 + Structure ctor (structure.cpp:7-20), as data extraction."""
+    lines = open(path).read().splitlines()
+    scale = float(lines[1].split()[0])
+    lat = np.array([[float(x) for x in lines[2 + i].split()[:3]] for i in range(3)]) * scale
+    counts = [int(x) for x in lines[6].split()]
+    direct = lines[7].strip()[:1] in ("d", "D")
+    n = sum(counts)
+    coords = np.array([[float(x) for x in lines[8 + i].split()[:3]] for i in range(n)])
+    species = np.concatenate([np.full(c, k, np.int32) for k, c in enumerate(counts)])
+    frac = coords if direct else coords @ np.linalg.inv(lat)
+    # pos = L^T * frac; Eigen fixed-size redux order x0 + (x1 + x2) (unpinned)
+    pos = np.empty((n, 3))
+    for k in range(3):
+        pos[:, k] = lat[0, k] * frac[:, 0] + (lat[1, k] * frac[:, 1] + lat[2, k] * frac[:, 2])
+    return lat, pos, species
+
+
+def betti_ref(lat, pos, species, rc):
+    f, c = O.ref_structure_betti(lat, pos, species, rc, omp_threads=8, ripser_threads=1)
+    f2, c2 = O.structure_betti(lat, pos, species, rc)
+    assert np.array_equal(c, c2), "restated reduction disagrees with verbatim Ripser"
+    assert np.allclose(f, f2, rtol=1e-12, atol=1e-12)
+    return f, c
+
+
+def main():
+    assert O.ref_available(), "build oracle/_ref first (make -C oracle)"
+    # (i) POSCARs: inputs + CSR at rc=5, K=12/20, RBF (rc=5, dr=0.1), Betti at rc=5
+    poscar = {}
+    for path in sorted(glob.glob(os.path.join(REF_POSCARS, "*.vasp"))):
+        name = os.path.basename(path)[:-5]
+        lat, pos, sp = parse_poscar(path)
+        poscar[f"{name}/lattice"] = lat
+        poscar[f"{name}/positions"] = pos
+        poscar[f"{name}/species"] = sp
+        for k in (12, 20):
+            nl = O.neighbor_list(lat, pos, 5.0, k)
+            poscar[f"{name}/k{k}/row_ptr"] = nl["row_ptr"]
+            poscar[f"{name}/k{k}/col"] = nl["col"]
+            poscar[f"{name}/k{k}/dist"] = nl["dist"]
+            if name in ("1", "741"):
+                poscar[f"{name}/k{k}/rbf"] = np.stack([O.gaussian_rbf(d, 5.0, 0.1) for d in nl["dist"]]).astype(
+                    np.float64)
+        if name in ("1", "741"):
+            f, c = betti_ref(lat, pos, sp, 5.0)
+            poscar[f"{name}/betti5/features"] = f
+            poscar[f"{name}/betti5/counts"] = c
+        print("poscar", name, pos.shape[0], "atoms")
+    np.savez_compressed(os.path.join(OUT, "poscar_rc5.npz"), **poscar)
+
+    # (ii) 8 jittered SC-64 cells: CSR K=20 + all-atom Betti (verbatim Ripser), local distances of 2 atoms
+    sc = {}
+    bt = synth.make_batch("sc", 4, 8)
+    n = 64
+    for s in range(8):
+        lat = bt["lattice"][s]
+        pos = bt["positions"][s * n:(s + 1) * n]
+        sp = bt["species"][s * n:(s + 1) * n]
+        nl = O.neighbor_list(lat, pos, 5.0, 20)
+        sc[f"{s}/row_ptr"] = nl["row_ptr"]
+        sc[f"{s}/col"] = nl["col"]
+        sc[f"{s}/dist"] = nl["dist"]
+        f, c = betti_ref(lat, pos, sp, 5.0)
+        sc[f"{s}/features"] = f
+        sc[f"{s}/counts"] = c
+        full = O.neighbor_list(lat, pos, 5.0, None)
+        for a in (0, 37):
+            r0, r1 = full["row_ptr"][a], full["row_ptr"][a + 1]
+            cloud = np.vstack([pos[a], pos[a] + full["disp"][r0:r1]])
+            sc[f"{s}/cloud{a}"] = cloud
+            sc[f"{s}/lower{a}"] = O.local_distances(cloud)
+            pr = O.ref_persistence(sc[f"{s}/lower{a}"], cloud.shape[0], np.float32(5.0))
+            for d in ("dim0", "dim1", "dim2"):
+                sc[f"{s}/pairs{a}/{d}"] = pr[d]
+        print("sc64", s)
+    np.savez_compressed(os.path.join(OUT, "sc64_rc5.npz"), **sc)
+
+    # (iii) known-answer tests, expected pairs from verbatim Ripser
+    kat = {}
+    clouds = {
+        "square": [[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]],
+        "octahedron": [[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]],
+        "cube": [[x, y, z] for x in (0, 1) for y in (0, 1) for z in (0, 1)],
+        "tetrahedron": [[1, 1, 1], [1, -1, -1], [-1, 1, -1], [-1, -1, 1]],
+        "hexagon": [[np.cos(k * np.pi / 3), np.sin(k * np.pi / 3), 0] for k in range(6)],
+        "two_points": [[0, 0, 0], [3, 0, 0]],
+        "duplicate": [[0, 0, 0], [0, 0, 0], [1, 0, 0]],
+    }
+    thresholds = {"octahedron_t15": 1.5}
+    for name, pts in list(clouds.items()) + [("octahedron_t15", clouds["octahedron"])]:
+        pts = np.asarray(pts, float)
+        if name == "tetrahedron":
+            pts = pts / np.sqrt(8.0)  # unit edge length
+        thr = np.float32(thresholds.get(name, 10.0))
+        low = O.local_distances(pts)
+        pr = O.ref_persistence(low, pts.shape[0], thr)
+        mine = O.persistence(low, pts.shape[0], thr)
+        for d in ("dim0", "dim1", "dim2"):
+            assert np.array_equal(pr[d], mine[d]), (name, d)
+        kat[f"{name}/cloud"] = pts
+        kat[f"{name}/threshold"] = np.float32(thr)
+        for d in ("dim0", "dim1", "dim2"):
+            kat[f"{name}/{d}"] = pr[d]
+        kat[f"{name}/n_inf0"] = np.int32(pr["n_inf0"])
+    np.savez_compressed(os.path.join(OUT, "kat.npz"), **kat)
+    for f in sorted(glob.glob(os.path.join(OUT, "*.npz"))):
+        print(f, os.path.getsize(f), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,93 @@
+"""HIP Betti path (MFMA distances + wave-parallel VR reduction + statistics) through the C ABI
+vs the oracle and the verbatim-Ripser golden fixtures. Counts and pairs bit-exact; the 35
+statistics within 1e-6 relative (absolute floor 1e-12: std of near-constant sets)."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLDEN
+
+import dgn
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+FEAT_RTOL, FEAT_ATOL = 1e-6, 1e-12
+
+
+def test_kat_pairs(ctx):
+    kat = np.load(os.path.join(GOLDEN, "kat.npz"))
+    names = sorted({k.split("/")[0] for k in kat.files})
+    for name in names:
+        pts = kat[f"{name}/cloud"]
+        thr = float(kat[f"{name}/threshold"])
+        pairs, counts = ctx.host_persistence(pts[None], [pts.shape[0]], thr, cap=64)
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            n = counts[0, [0, 2, 3][di]]
+            assert np.array_equal(pairs[0, di, :n], kat[f"{name}/{d}"]), (name, d, pairs[0, di, :n])
+        assert counts[0, 1] == int(kat[f"{name}/n_inf0"]), name
+
+
+def test_random_clouds_pairs_exact(ctx):
+    rng = np.random.default_rng(5)
+    C, maxp = 300, 48
+    clouds = np.zeros((C, maxp, 3))
+    npts = rng.integers(2, maxp + 1, size=C).astype(np.int32)
+    thr = 2.5
+    for c in range(C):
+        if c % 4 == 0:
+            clouds[c, :npts[c]] = rng.integers(0, 3, size=(npts[c], 3))  # exact ties
+        else:
+            clouds[c, :npts[c]] = rng.uniform(0, 4, size=(npts[c], 3))
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=512)
+    bad = []
+    for c in range(C):
+        n = npts[c]
+        low = O.local_distances(clouds[c, :n])
+        r = O.persistence(low, n, np.float32(thr))
+        got = {"dim0": pairs[c, 0, :counts[c, 0]], "dim1": pairs[c, 1, :counts[c, 2]], "dim2": pairs[c, 2, :counts[c, 3]]}
+        ok = all(np.array_equal(got[d], r[d]) for d in got) and counts[c, 1] == r["n_inf0"]
+        if not ok:
+            bad.append((c, n, counts[c].tolist(), [len(r[d]) for d in ("dim0", "dim1", "dim2")], r["n_inf0"]))
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("s", range(8))
+def test_sc64_fixture(ctx, s):
+    fx = np.load(os.path.join(GOLDEN, "sc64_rc5.npz"))
+    batch = dgn.synth_batch("sc", 4, 8)
+    n = 64
+    one = {"lattice": batch["lattice"][s:s + 1].copy(), "positions": batch["positions"][s * n:(s + 1) * n].copy(),
+           "species": batch["species"][s * n:(s + 1) * n].copy(), "atom_offset": np.array([0, n], np.int64)}
+    f, c = ctx.host_betti(one, 5.0)
+    assert np.array_equal(c, fx[f"{s}/counts"]), np.argwhere(c != fx[f"{s}/counts"])[:5]
+    np.testing.assert_allclose(f, fx[f"{s}/features"], rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
+@pytest.mark.parametrize("name", ["1", "741"])
+def test_poscar_fixture(ctx, name):
+    fx = np.load(os.path.join(GOLDEN, "poscar_rc5.npz"))
+    pos = fx[f"{name}/positions"]
+    one = {"lattice": fx[f"{name}/lattice"][None].copy(), "positions": pos.copy(),
+           "species": fx[f"{name}/species"].astype(np.int32), "atom_offset": np.array([0, len(pos)], np.int64)}
+    f, c = ctx.host_betti(one, 5.0)
+    assert np.array_equal(c, fx[f"{name}/betti5/counts"])
+    np.testing.assert_allclose(f, fx[f"{name}/betti5/features"], rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
+def test_fcc256_batch_vs_oracle(ctx):
+    batch = dgn.synth_batch("fcc", 4, 3)
+    f, c = ctx.host_betti(batch, 5.0)
+    n = 256
+    for s in range(3):
+        sl = slice(s * n, (s + 1) * n)
+        fo, co = O.structure_betti(batch["lattice"][s], batch["positions"][sl], batch["species"][sl], 5.0)
+        assert np.array_equal(c[sl], co)
+        np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
+def test_isolated_atom(ctx):
+    one = {"lattice": np.eye(3)[None] * 30.0, "positions": np.array([[1.0, 1.0, 1.0], [15.0, 15.0, 15.0]]),
+           "species": np.array([0, 1], np.int32), "atom_offset": np.array([0, 2], np.int64)}
+    f, c = ctx.host_betti(one, 5.0)
+    assert np.all(f == 0.0)
+    assert c.tolist() == [[0, 1, 0, 0], [0, 1, 0, 0]]

@@ -1,0 +1,111 @@
+"""HIP neighbour search + CSR + RBF through the C ABI vs the CPU oracle (bit-exact CSR and
+distances; RBF within 1e-6 relative as north_star states)."""
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLDEN
+
+import dgn
+import oracle_py as O
+from dgn import abi
+
+pytestmark = pytest.mark.gpu
+
+RBF_RTOL = 1e-6  # north_star: RBF/distance floats within 1e-6 relative
+
+
+def oracle_batch_csr(batch, rc, k):
+    rp_all, col_all, dist_all, disp_all = [np.zeros(1, np.int64)], [], [], []
+    off = batch["atom_offset"]
+    base = 0
+    for s in range(len(off) - 1):
+        a, b = off[s], off[s + 1]
+        nl = O.neighbor_list(batch["lattice"][s], batch["positions"][a:b], rc, k)
+        rp_all.append(nl["row_ptr"][1:] + base)
+        base += nl["row_ptr"][-1]
+        col_all.append(nl["col"])
+        dist_all.append(nl["dist"])
+        disp_all.append(nl["disp"])
+    return (np.concatenate(rp_all), np.concatenate(col_all), np.concatenate(dist_all), np.concatenate(disp_all))
+
+
+def check_rbf(rbf, dist, rc, dr):
+    ref = np.stack([O.gaussian_rbf(d, rc, dr) for d in dist])
+    rel = np.abs(rbf.astype(np.float64) - ref) / np.abs(ref)
+    assert rel.max() < RBF_RTOL, rel.max()
+
+
+@pytest.mark.parametrize("k", [20, 12, None])
+def test_sc64_batch(ctx, k):
+    batch = dgn.synth_batch("sc", 4, 16)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=k, rbf_cutoff=5.0, rbf_dr=0.1, write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, 5.0, k)
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)  # bit-exact: same op order, correctly rounded sqrt
+    assert np.array_equal(g["disp"], disp)
+    check_rbf(g["rbf"], dist, 5.0, 0.1)
+
+
+def test_fcc256_rbf_f64_default_cutoff(ctx):
+    batch = dgn.synth_batch("fcc", 4, 4)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=10.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F64)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, _ = oracle_batch_csr(batch, 5.0, 20)
+    assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
+    assert g["rbf"].shape == (len(dist), 100)
+    ref = np.stack([O.gaussian_rbf(d, 10.0, 0.1) for d in dist])
+    np.testing.assert_allclose(g["rbf"], ref, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("name", ["1", "1_1", "1_2", "741", "741_1", "741_2", "1046", "1046_1", "1046_2"])
+@pytest.mark.parametrize("k", [12, 20])
+def test_poscar_fixtures(ctx, name, k):
+    fx = np.load(os.path.join(GOLDEN, "poscar_rc5.npz"))
+    batch = {"lattice": fx[f"{name}/lattice"][None].copy(), "positions": fx[f"{name}/positions"].copy(),
+             "species": fx[f"{name}/species"].astype(np.int32), "atom_offset": np.array([0, len(fx[f"{name}/positions"])], np.int64)}
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=k, rbf_cutoff=5.0, rbf_dr=0.1)
+    g = ctx.host_graph(batch, p)
+    rp = fx[f"{name}/k{k}/row_ptr"]
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["dist"], fx[f"{name}/k{k}/dist"])
+    # CSR indices bit-exact; rows with exact distance ties compare as multisets (tie order is
+    # implementation-defined in the reference)
+    col, ref_col, d = g["col"], fx[f"{name}/k{k}/col"], fx[f"{name}/k{k}/dist"]
+    for i in range(len(rp) - 1):
+        a, b = rp[i], rp[i + 1]
+        if np.array_equal(col[a:b], ref_col[a:b]):
+            continue
+        assert sorted(zip(d[a:b], col[a:b])) == sorted(zip(d[a:b], ref_col[a:b])), (name, i)
+    if name in ("1", "741"):
+        np.testing.assert_allclose(g["rbf"], fx[f"{name}/k{k}/rbf"], rtol=RBF_RTOL, atol=0)
+
+
+def test_supercell_4096(ctx):
+    batch = dgn.synth_batch("sc", 16, 1)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, _ = oracle_batch_csr(batch, 5.0, 20)
+    assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
+
+
+def test_empty_and_ragged(ctx):
+    # structures of different sizes in one batch, including a 1-atom cell with no neighbours
+    a = dgn.synth_batch("sc", 2, 1)
+    b = dgn.synth_batch("fcc", 2, 1)
+    lone = {"lattice": np.eye(3)[None] * 20.0, "positions": np.array([[1.0, 2.0, 3.0]]),
+            "species": np.zeros(1, np.int32)}
+    parts = [a, lone, b]
+    batch = {"lattice": np.concatenate([x["lattice"] for x in parts]),
+             "positions": np.concatenate([x["positions"] for x in parts]),
+             "species": np.concatenate([x["species"] for x in parts]).astype(np.int32)}
+    sizes = [len(x["positions"]) for x in parts]
+    batch["atom_offset"] = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=None, rbf_cutoff=5.0, rbf_dr=0.1)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, _ = oracle_batch_csr(batch, 5.0, None)
+    assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
+    lone_row = sizes[0]
+    assert rp[lone_row + 1] - rp[lone_row] == 0
