@@ -26,8 +26,22 @@ $(LIB): $(KOBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# diagnostics variant: per-phase cycle stamps in the Betti kernel (never used by bench/tests)
+DBUILD := $(PKG)/build_diag
+DIAG   := $(PKG)/lib/libdgn_diag.so
+diag: $(DIAG)
+$(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
+	@mkdir -p $(DBUILD)
+	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING -c $< -o $@
+$(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp
+	@mkdir -p $(DBUILD)
+	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING -x hip -c $< -o $@
+$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/dgn_api.o
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
 clean:
-	rm -rf $(BUILD) $(LIB)
+	rm -rf $(BUILD) $(LIB) $(DBUILD) $(DIAG)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean diag

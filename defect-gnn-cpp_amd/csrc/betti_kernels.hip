@@ -16,29 +16,36 @@
 //     bit-identical to the reference's Eigen/SSE2 arithmetic;
 //   * dim 0: Prim on F-keys (diameter, then combinatorial index descending) == Kruskal's unique
 //     minimum spanning forest in Ripser's order (ripser.cpp:725-762);
-//   * dim 1 and dim 2: cohomology with clearing. Every column's pivot is found lane-parallel and
-//     apparent pairs (sigma youngest facet of tau, tau oldest cofacet of sigma) are settled in
-//     one pass; the few remaining columns are reduced in Ripser's column order by the whole
-//     wave, with Z/2 column additions as sorted-key symmetric differences (binary-search merge
-//     in LDS) and owner lookups that re-derive apparent owners on the fly. The persistence
-//     pairing of a total order is unique, so the emitted (birth, death) multiset equals the
-//     lock-free Ripser's (death > birth only; essential dim>=1 classes not emitted).
+//   * dim 1 and dim 2: cohomology with clearing. One lane per column finds its pivot (F-minimal
+//     cofacet) and settles apparent pairs (sigma youngest facet of tau, tau oldest cofacet of
+//     sigma). The wave then walks the remaining columns in Ripser's column order. A column is
+//     carried as its V list (the set of column simplices summed into it, Ripser's reduction
+//     matrix) with a membership bitmap in LDS; its pivot is recomputed lane-parallel as the
+//     F-minimal cofacet of odd multiplicity over the coboundaries of V (no sorting, no merging).
+//     Owners are looked up in a pivot table (serially resolved columns) or re-derived on the fly
+//     (apparent pairs). The persistence pairing of a total order is unique, so the emitted
+//     (birth, death) multiset equals the lock-free Ripser's (death > birth only; essential
+//     dim>=1 classes are not emitted, ripser.cpp:1209-1225).
 //   * persistent grid, chunked dynamic dequeue; per-wave global scratch for reduced columns
 //     and pair lists.
 #include "dgn_internal.hpp"
 
 namespace dgn {
 
-constexpr int kWCap = 256;        // working-column keys (LDS)
-constexpr int kNACap = 512;       // non-apparent columns per dimension (scratch)
-constexpr int kPivCap = 256;      // serially reduced pivots per dimension (LDS keys)
-constexpr int kPairCap = 1024;    // pairs per dimension (scratch)
-constexpr int kRCap = 8192;       // reduced-column keys per dimension (scratch)
+constexpr int kVCap = 256;        // simplices in one column's V list
+constexpr int kVStoreLds = 512;   // stored V-list entries kept in LDS (rest in scratch)
+constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
+constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
+constexpr int kPivLds = 128;      // serially resolved pivots kept in LDS (rest in scratch)
+constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
+constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
 constexpr int kChunk = 4;         // complexes per dequeue
 
 constexpr uint64_t kInf = ~0ull;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kLazyBit = 0x80000000u;  // vmeta: V = {column simplex} (packed in the low bits)
 
-// error bits
+// error bits (mirrored in dgn_api.cpp)
 constexpr uint32_t kErrTooManyPoints = 1u << 0;
 constexpr uint32_t kErrWorkCol = 1u << 1;
 constexpr uint32_t kErrNA = 1u << 2;
@@ -49,12 +56,16 @@ constexpr uint32_t kErrOrder = 1u << 6;
 
 // scratch layout per wave (bytes)
 struct ScratchLayout {
-    static constexpr int64_t na = 0;                                  // uint64 [kNACap]
-    static constexpr int64_t rmeta = na + 8 * kNACap;                // uint32 [kPivCap] (off<<12|len)
-    static constexpr int64_t p1 = rmeta + 4 * kPivCap;               // float2 [kPairCap]
+    static constexpr int64_t na_key = 0;                             // uint64 [kNACap] (unsorted)
+    static constexpr int64_t na_tau = na_key + 8 * kNACap;           // uint64 [kNACap]
+    static constexpr int64_t sna_key = na_tau + 8 * kNACap;          // sorted copies
+    static constexpr int64_t sna_tau = sna_key + 8 * kNACap;
+    static constexpr int64_t vmeta = sna_tau + 8 * kNACap;           // uint32 [kPivCap]
+    static constexpr int64_t piv = vmeta + 4 * kPivCap;              // uint64 [kPivCap]
+    static constexpr int64_t p1 = piv + 8 * kPivCap;                 // float2 [kPairCap]
     static constexpr int64_t p2 = p1 + 8 * kPairCap;                 // float2 [kPairCap]
-    static constexpr int64_t r = p2 + 8 * kPairCap;                  // uint64 [kRCap]
-    static constexpr int64_t total = r + 8 * kRCap;
+    static constexpr int64_t vstore = p2 + 8 * kPairCap;             // uint32 [kVStoreCap]
+    static constexpr int64_t total = vstore + 4 * kVStoreCap;
 };
 
 template <int NP>
@@ -64,60 +75,63 @@ struct BettiSmem {
     uint64_t tree[NP];
     uint16_t edges[NP * (NP - 1) / 2];
     uint32_t cleared[(NP * (NP - 1) * (NP - 2) / 6 + 31) / 32];
+    uint32_t vbits[(NP * (NP - 1) * (NP - 2) / 6 + 31) / 32];  // V membership (edges or triangles)
     union {
         struct {
             double X[NP][3];
             double sq[NP];
         } cloud;
-        struct {
-            uint64_t A[kWCap];  // working column / merge buffers
-            uint64_t B[kWCap];
-            uint64_t C[kWCap];
-        } col;
+        uint64_t sort_keys[kVStoreLds / 2];
+        uint32_t vstore[kVStoreLds];
     } u;
-    uint64_t piv[kPivCap];
+    uint32_t vcur[kVCap];
+    uint64_t piv[kPivLds];
+    uint32_t vmeta[kPivLds];
     float d0[NP];
 };
 
 // ---------------------------------------------------------------------------------------
 // small helpers
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, kWave);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, kWave);
-    return ((uint64_t)hi << 32) | lo;
-}
+// One-wave workgroups: a wave's LDS instructions execute in order, so lane-to-lane hand-offs
+// through LDS need only a compiler barrier. __syncthreads() would add a workgroup release
+// fence (s_waitcnt vmcnt(0)) that stalls on every in-flight global load/store; it is kept only
+// where data passes between lanes through global scratch.
+__device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
     return ((uint64_t)hi << 32) | lo;
 }
+// min over the wave of a 64-bit key, DPP row rotations (VALU latency) + 4 readlanes
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = shfl_xor64(v, o);
-        v = w < v ? w : v;
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define DGN_MIN_STEP(ctrl)                                                          \
+    {                                                                               \
+        const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, ctrl, 0xf, 0xf, false); \
+        const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, ctrl, 0xf, 0xf, false); \
+        const bool take = (h2 < hi) || (h2 == hi && l2 < lo);                       \
+        lo = take ? l2 : lo;                                                        \
+        hi = take ? h2 : hi;                                                        \
     }
-    return v;
-}
-// ascending bitonic sort of one key per lane (kInf pads)
-__device__ __forceinline__ uint64_t wave_sort_u64(uint64_t key) {
-    const int lane = lane_id();
+    DGN_MIN_STEP(0x121)  // row_ror:1
+    DGN_MIN_STEP(0x122)  // row_ror:2
+    DGN_MIN_STEP(0x124)  // row_ror:4
+    DGN_MIN_STEP(0x128)  // row_ror:8
+#undef DGN_MIN_STEP
+    uint64_t best = kInf;
 #pragma unroll
-    for (int k = 2; k <= kWave; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t other = shfl_xor64(key, j);
-            const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
-            const uint64_t mn = other < key ? other : key;
-            const uint64_t mx = other < key ? key : other;
-            key = keep_min ? mn : mx;
-        }
+    for (int r = 0; r < 4; ++r) {
+        const uint64_t x = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
+        best = x < best ? x : best;
     }
-    return key;
+    return best;
 }
-__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) { return (uint32_t)__shfl((int)v, l, kWave); }
 
+// F-order key: ascending key == Ripser's filtration order (diameter ascending, then the
+// combinatorial index DESCENDING, greater_diameter_or_smaller_index at ripser.cpp:318-324).
+// Vertex tuples packed 8 bits per vertex in descending order preserve the colex (index) order.
 __device__ __forceinline__ uint64_t make_key(float diam, uint32_t packed) {
     return ((uint64_t)__float_as_uint(diam) << 32) | (uint64_t)(~packed);
 }
@@ -131,70 +145,28 @@ __device__ __forceinline__ uint32_t pack3(int a, int b, int c) {
 __device__ __forceinline__ uint32_t pack4(int a, int b, int c, int d) {
     return ((uint32_t)a << 24) | ((uint32_t)b << 16) | ((uint32_t)c << 8) | (uint32_t)d;
 }
-// insert k into descending (a,b) -> packed descending triple
-__device__ __forceinline__ uint32_t tri_with(int a, int b, int k) {
+__device__ __forceinline__ uint32_t tri_with(int a, int b, int k) {  // a > b; insert k
     return k > a ? pack3(k, a, b) : (k > b ? pack3(a, k, b) : pack3(a, b, k));
 }
-__device__ __forceinline__ uint32_t tet_with(int a, int b, int c, int k) {
+__device__ __forceinline__ uint32_t tet_with(int a, int b, int c, int k) {  // a > b > c; insert k
     return k > a ? pack4(k, a, b, c) : k > b ? pack4(a, k, b, c) : k > c ? pack4(a, b, k, c) : pack4(a, b, c, k);
 }
 __device__ __forceinline__ int tri_dense(int a, int b, int c) {  // combinatorial index, a > b > c
     return a * (a - 1) * (a - 2) / 6 + b * (b - 1) / 2 + c;
 }
-
-// number of elements < key in sorted arr[0..n)
-__device__ __forceinline__ int lower_bound_u64(const uint64_t* arr, int n, uint64_t key) {
-    int lo = 0, len = n;
-    while (len > 0) {
-        const int half = len >> 1;
-        if (arr[lo + half] < key) {
-            lo += half + 1;
-            len -= half + 1;
-        } else {
-            len = half;
-        }
-    }
-    return lo;
+__device__ __forceinline__ int edge_dense(int a, int b) { return a * (a - 1) / 2 + b; }  // a > b
+// dense combinatorial index of a packed column simplex (edge for dim 1, triangle for dim 2)
+__device__ __forceinline__ int col_dense(int dim, uint32_t p) {
+    return dim == 1 ? edge_dense((p >> 8) & 255, p & 255) : tri_dense((p >> 16) & 255, (p >> 8) & 255, p & 255);
 }
-
-// out = A xor B (sorted symmetric difference), returns length (or -1 on overflow).
-__device__ int merge_xor(const uint64_t* A, int na, const uint64_t* B, int nb, uint64_t* out) {
-    const int lane = lane_id();
-    int survA = 0, survB = 0;
-    // first count survivors of both to know the output length
-    int outlen = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint64_t* S = pass == 0 ? A : B;
-        const uint64_t* O = pass == 0 ? B : A;
-        const int ns = pass == 0 ? na : nb, no = pass == 0 ? nb : na;
-        int carry = 0;
-        for (int base = 0; base < ns; base += kWave) {
-            const int i = base + lane;
-            bool surv = false;
-            int lb = 0;
-            uint64_t v = 0;
-            if (i < ns) {
-                v = S[i];
-                lb = lower_bound_u64(O, no, v);
-                surv = !(lb < no && O[lb] == v);
-            }
-            const uint64_t bal = ballot(surv);
-            const int sp = carry + mask_prefix(bal);  // survivors of S before i
-            if (surv) {
-                const int pos = sp + lb - (i - sp);
-                if (pos < kWCap) out[pos] = v;
-            }
-            carry += __popcll(bal);
-        }
-        if (pass == 0) survA = carry;
-        else survB = carry;
-    }
-    outlen = survA + survB;
-    return outlen <= kWCap ? outlen : -1;
+__device__ __forceinline__ uint32_t sort2(int a, int b) { return a > b ? pack2(a, b) : pack2(b, a); }
+__device__ __forceinline__ uint32_t sort3(int a, int b, int c) {  // any order -> packed descending
+    const int hi = max(a, max(b, c)), lo = min(a, min(b, c)), mid = a + b + c - hi - lo;
+    return pack3(hi, mid, lo);
 }
 
 // ---------------------------------------------------------------------------------------
-// the kernel
+// one local complex
 // ---------------------------------------------------------------------------------------
 template <int NP>
 struct Complex {
@@ -205,18 +177,14 @@ struct Complex {
     uint32_t err;
     // pair counts (wave-uniform)
     int n_d0, n_inf0, n_p1, n_p2;
+    int n_adds, n_spills;  // diagnostics
 
-    __device__ float dist(int a, int b) const { return s.D[a][b]; }
     __device__ uint64_t ekey(int i, int j) const {  // i != j
         const int a = i > j ? i : j, b = i > j ? j : i;
         return make_key(s.D[a][b], pack2(a, b));
     }
-    __device__ float tri_diam(int a, int b, int c) const {
-        return fmaxf(fmaxf(s.D[a][b], s.D[a][c]), s.D[b][c]);
-    }
-    __device__ uint64_t tkey(int a, int b, int c) const {  // a > b > c
-        return make_key(tri_diam(a, b, c), pack3(a, b, c));
-    }
+    __device__ float tri_diam(int a, int b, int c) const { return fmaxf(fmaxf(s.D[a][b], s.D[a][c]), s.D[b][c]); }
+    __device__ uint64_t tkey(int a, int b, int c) const { return make_key(tri_diam(a, b, c), pack3(a, b, c)); }
     __device__ bool is_cleared(int a, int b, int c) const {
         const int t = tri_dense(a, b, c);
         return (s.cleared[t >> 5] >> (t & 31)) & 1u;
@@ -225,12 +193,10 @@ struct Complex {
         const int t = tri_dense(a, b, c);
         atomicOr(&s.cleared[t >> 5], 1u << (t & 31));
     }
-    __device__ uint64_t* na_list() { return reinterpret_cast<uint64_t*>(scratch + ScratchLayout::na); }
-    __device__ uint32_t* rmeta() { return reinterpret_cast<uint32_t*>(scratch + ScratchLayout::rmeta); }
-    __device__ float2* pairs(int dim) {
-        return reinterpret_cast<float2*>(scratch + (dim == 1 ? ScratchLayout::p1 : ScratchLayout::p2));
-    }
-    __device__ uint64_t* rstore() { return reinterpret_cast<uint64_t*>(scratch + ScratchLayout::r); }
+    template <typename T>
+    __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scratch + off); }
+    __device__ float2* pairs(int dim) const { return sp<float2>(dim == 1 ? ScratchLayout::p1 : ScratchLayout::p2); }
+    __device__ bool vbit(int idx) const { return (s.vbits[idx >> 5] >> (idx & 31)) & 1u; }
 
     // wave-uniform: append pairs (birth, death) for lanes with `emit`
     __device__ void append_pairs(int dim, bool emit, float birth, float death) {
@@ -243,179 +209,332 @@ struct Complex {
         np += __popcll(bal);
     }
 
-    // F-min cofacet (key) of the simplex with vertex tuple v (dim = 1 edge, 2 triangle) over
-    // candidate mask cand, whole wave: lane k evaluates vertex k.
-    __device__ uint64_t min_cofacet_wave(int dim, int a, int b, int c, float diam, uint64_t cand) const {
-        const int k = lane_id();
-        uint64_t key = kInf;
-        if ((cand >> k) & 1ull) {
-            if (dim == 1) {
-                const float dd = fmaxf(diam, fmaxf(s.D[a][k], s.D[b][k]));
-                key = make_key(dd, tri_with(a, b, k));
-            } else {
-                const float dd = fmaxf(diam, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k]));
-                key = make_key(dd, tet_with(a, b, c, k));
+    // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand
+    __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, float diam, uint64_t cand) const {
+        uint64_t best = kInf;
+        while (cand) {
+            int ks[4];
+            int m = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                ks[u] = cand ? __ffsll((unsigned long long)cand) - 1 : 0;
+                if (cand) {
+                    cand &= cand - 1;
+                    ++m;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (u < m) {
+                    const int k = ks[u];
+                    uint64_t key;
+                    if (dim == 1) key = make_key(fmaxf(diam, fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
+                    else key = make_key(fmaxf(diam, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k])), tet_with(a, b, c, k));
+                    best = key < best ? key : best;
+                }
             }
         }
-        return wave_min_u64(key);
+        return best;
     }
 
-    // Sorted coboundary of a column simplex into out (whole wave); returns length.
-    __device__ int coboundary_sorted(int dim, int a, int b, int c, uint64_t* out) const {
+    // whole wave: F-minimal cofacet, lane k evaluates vertex k
+    __device__ uint64_t min_cofacet_wave(int dim, int a, int b, int c, float diam, uint64_t cand) const {
         const int k = lane_id();
-        uint64_t cand;
-        float diam;
-        if (dim == 1) {
-            cand = s.adj[a] & s.adj[b];
-            diam = s.D[a][b];
-        } else {
-            cand = s.adj[a] & s.adj[b] & s.adj[c];
-            diam = tri_diam(a, b, c);
-        }
         uint64_t key = kInf;
         if ((cand >> k) & 1ull) {
             if (dim == 1) key = make_key(fmaxf(diam, fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
             else key = make_key(fmaxf(diam, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k])), tet_with(a, b, c, k));
         }
-        key = wave_sort_u64(key);
-        const int len = __popcll(cand);
-        if (k < len) out[k] = key;
-        return len;
+        return wave_min_u64(key);
     }
 
-    // If the pivot simplex tau (dim+1) is the pivot of an apparent pair, return the owner's
-    // packed column vertices (dim simplex) else 0xFFFFFFFF. Whole wave.
-    __device__ uint32_t apparent_owner(int dim, uint64_t tau) const {
+    // F-max facet of pivot tau as (packed vertices); owner iff it is a column (not a tree edge,
+    // not cleared) whose F-min cofacet is tau (apparent pair)
+    __device__ uint32_t max_facet(int dim, uint64_t tau, bool& is_column) const {
         const uint32_t p = key_packed(tau);
         if (dim == 1) {
             const int a = (p >> 16) & 255, b = (p >> 8) & 255, c = p & 255;
-            // F-max facet among (a,b), (a,c), (b,c)
-            uint64_t k0 = ekey(a, b), k1 = ekey(a, c), k2 = ekey(b, c);
+            uint64_t best = ekey(a, b);
             int fa = a, fb = b;
-            uint64_t best = k0;
-            if (k1 > best) { best = k1; fa = a; fb = c; }
-            if (k2 > best) { best = k2; fa = b; fb = c; }
-            if ((s.tree[fa] >> fb) & 1ull) return 0xFFFFFFFFu;  // tree edges are not columns
-            const uint64_t m = min_cofacet_wave(1, fa, fb, 0, s.D[fa][fb], s.adj[fa] & s.adj[fb]);
-            return m == tau ? pack2(fa, fb) : 0xFFFFFFFFu;
+            uint64_t k = ekey(a, c);
+            if (k > best) { best = k; fa = a; fb = c; }
+            k = ekey(b, c);
+            if (k > best) { best = k; fa = b; fb = c; }
+            is_column = !((s.tree[fa] >> fb) & 1ull);
+            return pack2(fa, fb);
         } else {
             const int a = (p >> 24) & 255, b = (p >> 16) & 255, c = (p >> 8) & 255, d = p & 255;
             uint64_t best = tkey(a, b, c);
             int fa = a, fb = b, fc = c;
-            uint64_t k;
-            k = tkey(a, b, d); if (k > best) { best = k; fa = a; fb = b; fc = d; }
-            k = tkey(a, c, d); if (k > best) { best = k; fa = a; fb = c; fc = d; }
-            k = tkey(b, c, d); if (k > best) { best = k; fa = b; fb = c; fc = d; }
-            if (is_cleared(fa, fb, fc)) return 0xFFFFFFFFu;
-            const uint64_t m = min_cofacet_wave(2, fa, fb, fc, tri_diam(fa, fb, fc), s.adj[fa] & s.adj[fb] & s.adj[fc]);
-            return m == tau ? pack3(fa, fb, fc) : 0xFFFFFFFFu;
+            uint64_t k = tkey(a, b, d);
+            if (k > best) { best = k; fa = a; fb = b; fc = d; }
+            k = tkey(a, c, d);
+            if (k > best) { best = k; fa = a; fb = c; fc = d; }
+            k = tkey(b, c, d);
+            if (k > best) { best = k; fa = b; fb = c; fc = d; }
+            is_column = !is_cleared(fa, fb, fc);
+            return pack3(fa, fb, fc);
         }
     }
+    __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
+        bool col;
+        const uint32_t f = max_facet(dim, tau, col);
+        if (!col) return kNone;
+        uint64_t m;
+        if (dim == 1) {
+            const int fa = (f >> 8) & 255, fb = f & 255;
+            m = min_cofacet_wave(1, fa, fb, 0, s.D[fa][fb], s.adj[fa] & s.adj[fb]);
+        } else {
+            const int fa = (f >> 16) & 255, fb = (f >> 8) & 255, fc = f & 255;
+            m = min_cofacet_wave(2, fa, fb, fc, tri_diam(fa, fb, fc), s.adj[fa] & s.adj[fb] & s.adj[fc]);
+        }
+        return m == tau ? f : kNone;
+    }
 
-    // Serial reduction of the non-apparent columns of one dimension (whole wave).
+    __device__ uint64_t column_key(int dim, uint32_t cp) const {
+        return dim == 1 ? ekey((cp >> 8) & 255, cp & 255) : tkey((cp >> 16) & 255, (cp >> 8) & 255, cp & 255);
+    }
+
+    // serially resolved pivot table: find tau (whole wave)
+    __device__ int find_pivot(int npiv, uint64_t tau) const {
+        const int lane = lane_id();
+        const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
+        for (int base = 0; base < npiv; base += kWave) {
+            const int i = base + lane;
+            bool hit = false;
+            if (i < npiv) hit = (i < kPivLds ? s.piv[i] : sp_piv[i]) == tau;
+            const uint64_t bal = ballot(hit);
+            if (bal) return base + __ffsll((unsigned long long)bal) - 1;
+        }
+        return -1;
+    }
+
+    // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
+    // multiplicity. Cofacet tau = s u {k} is evaluated by lane k for each s in V; its other
+    // facets are found in V through the LDS bitmap, and only the packed-smallest facet of tau
+    // in V reports it (so each tau is counted once). kInf for the zero column.
+    __device__ uint64_t pivot_of_V(int dim, int v) const {
+        const int k = lane_id();
+        uint64_t best = kInf;
+        for (int i = 0; i < v; ++i) {
+            const uint32_t sp_ = s.vcur[i];
+            if (dim == 1) {
+                const int a = (sp_ >> 8) & 255, b = sp_ & 255;
+                const uint64_t cand = s.adj[a] & s.adj[b];
+                if ((cand >> k) & 1ull) {
+                    const uint32_t f1 = sort2(a, k), f2 = sort2(b, k);
+                    const bool m1 = vbit(col_dense(1, f1)), m2 = vbit(col_dense(1, f2));
+                    const bool odd = !(m1 ^ m2);  // 1 + m1 + m2 odd
+                    const bool rep = !(m1 && f1 < sp_) && !(m2 && f2 < sp_);
+                    if (odd && rep) {
+                        const uint64_t key = make_key(fmaxf(s.D[a][b], fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
+                        best = key < best ? key : best;
+                    }
+                }
+            } else {
+                const int a = (sp_ >> 16) & 255, b = (sp_ >> 8) & 255, c = sp_ & 255;
+                const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
+                if ((cand >> k) & 1ull) {
+                    const uint32_t f1 = sort3(a, b, k), f2 = sort3(a, c, k), f3 = sort3(b, c, k);
+                    const bool m1 = vbit(col_dense(2, f1)), m2 = vbit(col_dense(2, f2)), m3 = vbit(col_dense(2, f3));
+                    const bool odd = !(m1 ^ m2 ^ m3);
+                    const bool rep = !(m1 && f1 < sp_) && !(m2 && f2 < sp_) && !(m3 && f3 < sp_);
+                    if (odd && rep) {
+                        const float dd = fmaxf(tri_diam(a, b, c), fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k]));
+                        const uint64_t key = make_key(dd, tet_with(a, b, c, k));
+                        best = key < best ? key : best;
+                    }
+                }
+            }
+        }
+        return wave_min_u64(best);
+    }
+
+    // V ^= {x}: toggle one simplex in the current V list (whole wave, uniform arguments)
+    __device__ bool v_toggle(int dim, uint32_t x, int& v) {
+        const int lane = lane_id();
+        const int idx = col_dense(dim, x);
+        if (vbit(idx)) {
+            int pos = -1;
+            for (int base = 0; base < v && pos < 0; base += kWave) {
+                const uint64_t bal = ballot(base + lane < v && s.vcur[base + lane] == x);
+                if (bal) pos = base + __ffsll((unsigned long long)bal) - 1;
+            }
+            const uint32_t last = s.vcur[v - 1];
+            lds_sync();
+            if (lane == 0) {
+                s.vcur[pos] = last;
+                atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
+            }
+            --v;
+        } else {
+            if (v >= kVCap) return false;
+            if (lane == 0) {
+                s.vcur[v] = x;
+                atomicOr(&s.vbits[idx >> 5], 1u << (idx & 31));
+            }
+            ++v;
+        }
+        lds_sync();
+        return true;
+    }
+
+    // Walk the non-apparent columns in Ripser's order (whole wave). na_* arrays hold each
+    // column's key and its unreduced pivot.
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
-        uint64_t* na = na_list();
-        // sort non-apparent columns by key DESCENDING (Ripser column order): rank sort
         if (nna > kNACap) { err |= kErrNA; return; }
-        // rank sort into the B buffer region of LDS is too small for kNACap; sort in scratch:
-        // simple odd-even pass over chunks is avoided — use rank counting over global memory.
-        uint64_t* sorted = rstore();  // temporarily use the R store head, then shift R below
-        for (int base = 0; base < nna; base += kWave) {
-            const int i = base + lane;
-            if (i < nna) {
-                const uint64_t v = na[i];
-                int rank = 0;
-                for (int u = 0; u < nna; ++u) rank += (na[u] > v);
-                sorted[rank] = v;
+        // ---- sort by column key DESCENDING (rank sort; keys staged in LDS when they fit) ----
+        {
+            uint64_t* keys = s.u.sort_keys;
+            const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
+            const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
+            uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
+            uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
+            const bool in_lds = nna <= kVStoreLds / 2;
+            if (in_lds) {
+                for (int i = lane; i < nna; i += kWave) keys[i] = gk[i];
+                lds_sync();
             }
+            for (int i = lane; i < nna; i += kWave) {
+                const uint64_t v = in_lds ? keys[i] : gk[i];
+                int rank = 0;
+                if (in_lds) {
+                    for (int u = 0; u < nna; ++u) rank += keys[u] > v;
+                } else {
+                    for (int u = 0; u < nna; ++u) rank += gk[u] > v;
+                }
+                sk[rank] = v;
+                st[rank] = gt[i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        for (int base = 0; base < nna; base += kWave) {
-            const int i = base + lane;
-            if (i < nna) na[i] = sorted[i];
-        }
-        __syncthreads();
-        int npiv = 0;
-        int rused = 0;
-        uint64_t* W = s.u.col.A;
-        uint64_t* T = s.u.col.B;
-        uint64_t* X = s.u.col.C;
+        const uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
+        const uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
+        uint32_t* gvmeta = sp<uint32_t>(ScratchLayout::vmeta);
+        uint64_t* gpiv = sp<uint64_t>(ScratchLayout::piv);
+        uint32_t* gvstore = sp<uint32_t>(ScratchLayout::vstore);
+        int npiv = 0, vused = 0;
+        uint64_t nk = nna > 0 ? sk[0] : 0, nt = nna > 0 ? st[0] : 0;
         for (int ci = 0; ci < nna; ++ci) {
-            const uint64_t colkey = na[ci];
+            const uint64_t colkey = nk;
+            uint64_t tau = nt;
+            if (ci + 1 < nna) {  // prefetch the next column's record
+                nk = sk[ci + 1];
+                nt = st[ci + 1];
+            }
             const uint32_t cp = key_packed(colkey);
             const float birth = key_diam(colkey);
-            int ca, cb, cc = 0;
-            if (dim == 1) { ca = (cp >> 8) & 255; cb = cp & 255; }
-            else { ca = (cp >> 16) & 255; cb = (cp >> 8) & 255; cc = cp & 255; }
-            int nw = coboundary_sorted(dim, ca, cb, cc, W);
-            __syncthreads();
-            int guard = 0;
-            while (true) {
-                if (nw == 0) break;  // essential class: not emitted (ripser.cpp:1209-1225)
-                const uint64_t tau = W[0];
-                // owner among serially reduced columns (LDS keys)
-                int owner = -1;
-                for (int base = 0; base < npiv; base += kWave) {
-                    const int i = base + lane;
-                    const bool hit = i < npiv && s.piv[i] == tau;
-                    const uint64_t bal = ballot(hit);
-                    if (bal) { owner = base + __ffsll((unsigned long long)bal) - 1; break; }
-                }
-                int nx = 0;
-                if (owner >= 0) {
-                    const uint32_t meta = rmeta()[owner];
-                    const int off = (int)(meta >> 12), len = (int)(meta & 4095);
-                    for (int i = lane; i < len; i += kWave) X[i] = rstore()[off + i];
-                    nx = len;
-                } else {
-                    const uint32_t ow = apparent_owner(dim, tau);
-                    if (ow == 0xFFFFFFFFu) {
-                        // tau is unowned: pivot of this column
-                        const float death = key_diam(tau);
-                        if (lane == 0 && death > birth) {
-                            const int slot = dim == 1 ? n_p1 : n_p2;
-                            if (slot < kPairCap) pairs(dim)[slot] = make_float2(birth, death);
+            int owner = find_pivot(npiv, tau);
+            uint32_t app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+            int v = 0;  // 0 = lazy: V == {this column}
+            if (owner >= 0 || app != kNone) {
+                v_toggle(dim, cp, v);
+                int guard = 0;
+                while (true) {
+                    // V ^= V(owner)
+                    bool ok = true;
+                    if (app != kNone) {
+                        // an apparent owner precedes this column in Ripser's order (key greater)
+                        if (!(column_key(dim, app) > colkey)) { err |= kErrOrder; return; }
+                        ok = v_toggle(dim, app, v);
+                    } else {
+                        const uint32_t m = owner < kPivLds ? s.vmeta[owner] : gvmeta[owner];
+                        if (m & kLazyBit) {
+                            ok = v_toggle(dim, m & ~kLazyBit, v);
+                        } else {
+                            const int off = (int)(m >> 9), len = (int)(m & 511);
+                            for (int t = 0; t < len && ok; ++t) {
+                                const uint32_t x = off + t < kVStoreLds ? s.u.vstore[off + t] : gvstore[off + t];
+                                ok = v_toggle(dim, x, v);
+                            }
                         }
-                        if (death > birth) { if (dim == 1) ++n_p1; else ++n_p2; }
-                        if (dim == 1 && lane == 0) {
-                            const uint32_t tp = key_packed(tau);
-                            set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
-                        }
-                        if (npiv >= kPivCap || rused + nw > kRCap) { err |= (npiv >= kPivCap ? kErrPiv : kErrR); return; }
-                        for (int i = lane; i < nw; i += kWave) rstore()[rused + i] = W[i];
-                        if (lane == 0) {
-                            s.piv[npiv] = tau;
-                            rmeta()[npiv] = ((uint32_t)rused << 12) | (uint32_t)nw;
-                        }
-                        rused += nw;
-                        ++npiv;
-                        __syncthreads();
-                        break;
                     }
-                    // owner must precede this column in Ripser's order (key greater)
-                    const uint64_t okey = dim == 1 ? ekey((ow >> 8) & 255, ow & 255)
-                                                   : tkey((ow >> 16) & 255, (ow >> 8) & 255, ow & 255);
-                    if (!(okey > colkey)) { err |= kErrOrder; return; }
-                    if (dim == 1) nx = coboundary_sorted(1, (ow >> 8) & 255, ow & 255, 0, X);
-                    else nx = coboundary_sorted(2, (ow >> 16) & 255, (ow >> 8) & 255, ow & 255, X);
+                    if (!ok) { err |= kErrWorkCol; return; }
+                    ++n_adds;
+                    tau = v > 0 ? pivot_of_V(dim, v) : kInf;
+                    if (tau == kInf) break;  // zero column: essential class, not emitted
+                    owner = find_pivot(npiv, tau);
+                    app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+                    if (owner < 0 && app == kNone) break;  // tau is this column's pivot
+                    if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
-                __syncthreads();
-                const int nt = merge_xor(W, nw, X, nx, T);
-                __syncthreads();
-                if (nt < 0) { err |= kErrWorkCol; return; }
-                uint64_t* tmp = W; W = T; T = tmp;
-                nw = nt;
-                if (++guard > 100000) { err |= kErrWorkCol; return; }
+                if (tau == kInf) {
+                    // clear the membership bits of the (zero) column's V
+                    for (int t = lane; t < v; t += kWave) {
+                        const int idx = col_dense(dim, s.vcur[t]);
+                        atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
+                    }
+                    lds_sync();
+                    continue;
+                }
             }
+            // ---- tau is the pivot of this column ----
+            const float death = key_diam(tau);
+            if (death > birth) {
+                if (lane == 0) {
+                    const int slot = dim == 1 ? n_p1 : n_p2;
+                    if (slot < kPairCap) pairs(dim)[slot] = make_float2(birth, death);
+                }
+                if (dim == 1) ++n_p1;
+                else ++n_p2;
+            }
+            if (dim == 1 && lane == 0) {
+                const uint32_t tp = key_packed(tau);
+                set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
+            }
+            if (npiv >= kPivCap) { err |= kErrPiv; return; }
+            uint32_t meta;
+            if (v == 0) {
+                meta = kLazyBit | cp;
+            } else {
+                if (vused + v > kVStoreCap || v > 511) { err |= kErrR; return; }
+                for (int t = lane; t < v; t += kWave) {
+                    const uint32_t x = s.vcur[t];
+                    if (vused + t < kVStoreLds) s.u.vstore[vused + t] = x;
+                    else gvstore[vused + t] = x;
+                    const int idx = col_dense(dim, x);
+                    atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
+                }
+                meta = ((uint32_t)vused << 9) | (uint32_t)v;
+                vused += v;
+            }
+            if (lane == 0) {
+                if (npiv < kPivLds) {
+                    s.piv[npiv] = tau;
+                    s.vmeta[npiv] = meta;
+                } else {
+                    gpiv[npiv] = tau;
+                    gvmeta[npiv] = meta;
+                }
+            }
+            ++npiv;
+            lds_sync();
         }
     }
 };
+
+#ifdef DGN_PHASE_TIMING
+#define DGN_PHASE(k)                                          \
+    do {                                                      \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        ph[k] += t_ - t_prev;                                 \
+        t_prev = t_;                                          \
+    } while (0)
+#else
+#define DGN_PHASE(k) \
+    do {             \
+    } while (0)
+#endif
 
 template <int NP>
 __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
     __shared__ int64_t chunk_s;
+#ifdef DGN_PHASE_TIMING
+    uint64_t ph[16] = {0};
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#endif
     const int lane = lane_id();
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;
@@ -429,7 +548,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
         for (int64_t gi = chunk0; gi < chunk0 + kChunk && gi < A; ++gi) {
             int64_t r0 = 0;
             int n;
-            if (bl.clouds) {
+            if (bl.clouds || bl.lower) {
                 n = bl.npoints[gi];
             } else {
                 r0 = bl.row_ptr[gi];
@@ -446,9 +565,9 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     else hi = mid - 1;
                 }
                 const int64_t s0 = bl.atom_offset[lo], s1 = bl.atom_offset[lo + 1];
-                const int sp = bl.species[gi];
+                const int spc = bl.species[gi];
                 int cnt = 0;
-                for (int64_t j = s0 + lane; j < s1; j += kWave) cnt += (bl.species[j] == sp);
+                for (int64_t j = s0 + lane; j < s1; j += kWave) cnt += (bl.species[j] == spc);
                 cnt = wave_sum(cnt);
                 weight = 1.0 / (double)cnt;
             }
@@ -459,7 +578,8 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
                 continue;
             }
-            Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0};
+            Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0, 0, 0};
+            DGN_PHASE(7);
             // ---- load the local cloud (betti_features.cpp:67-73) ----
             if (lane < n && bl.clouds) {
                 const double* xc = bl.clouds + ((int64_t)gi * bl.cloud_stride + lane) * 3;
@@ -467,7 +587,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 s.u.cloud.X[lane][1] = xc[1];
                 s.u.cloud.X[lane][2] = xc[2];
                 s.u.cloud.sq[lane] = (xc[0] * xc[0] + xc[1] * xc[1]) + xc[2] * xc[2];
-            } else if (lane < n) {
+            } else if (lane < n && !bl.lower) {
                 const double* q = bl.pos + 3 * gi;
                 double x[3];
                 if (lane == 0) {
@@ -482,9 +602,22 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 // rowwise().squaredNorm(): (x0^2 + x1^2) + x2^2
                 s.u.cloud.sq[lane] = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
             }
-            __syncthreads();
+            lds_sync();
             // ---- distance matrix on the matrix cores (ripser_wrapper.cpp:64-67) ----
-            {
+            if (bl.lower) {
+                // given f32 lower triangle (ripser_wrapper.cpp:20-24 packing)
+                const float* L = bl.lower + (int64_t)gi * ((int64_t)bl.cloud_stride * (bl.cloud_stride - 1) / 2);
+                const int tot = n * (n - 1) / 2;
+                for (int t = lane; t < tot; t += kWave) {
+                    int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
+                    while (i * (i - 1) / 2 > t) --i;
+                    while ((i + 1) * i / 2 <= t) ++i;
+                    const int j = t - i * (i - 1) / 2;
+                    s.D[i][j] = L[t];
+                    s.D[j][i] = L[t];
+                }
+                if (lane < n) s.D[lane][lane] = 0.0f;
+            } else {
                 typedef double double4_t __attribute__((ext_vector_type(4)));
                 const int T = (n + 15) / 16;
                 const int kk = lane >> 4;
@@ -514,7 +647,8 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     }
                 }
             }
-            __syncthreads();
+            lds_sync();
+            DGN_PHASE(0);
             // ---- adjacency (sparse_distance_matrix: i != j and d <= thr, ripser.cpp:386-395) ----
             {
                 uint64_t m = 0;
@@ -525,8 +659,11 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 s.adj[lane] = lane < n ? m : 0ull;
                 s.tree[lane] = 0ull;
             }
-            for (int i = lane; i < (int)(sizeof(s.cleared) / 4); i += kWave) s.cleared[i] = 0u;
-            __syncthreads();
+            for (int i = lane; i < (int)(sizeof(s.cleared) / 4); i += kWave) {
+                s.cleared[i] = 0u;
+                s.vbits[i] = 0u;
+            }
+            lds_sync();
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
             cx.n_d0 = 0;
@@ -568,7 +705,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     }
                 }
             }
-            __syncthreads();
+            lds_sync();
             // ---- edge list (i > j, d <= thr), row-major ----
             int n_edges = 0;
             {
@@ -584,37 +721,32 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     s.edges[off++] = (uint16_t)((lane << 8) | j);
                 }
             }
-            __syncthreads();
+            lds_sync();
             cx.n_p1 = 0;
             cx.n_p2 = 0;
-            // ---- dim 1 ----
+            DGN_PHASE(1);
+            uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
+            uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
+                    // ---- dim 1: one lane per column (non-tree edge) ----
             if (dim_max >= 1) {
                 int nna = 0;
                 for (int base = 0; base < n_edges; base += kWave) {
                     const int e = base + lane;
-                    bool is_col = false, apparent = false, na_col = false;
+                    bool apparent = false, na_col = false;
                     float birth = 0.f, death = 0.f;
-                    uint64_t colkey = 0;
+                    uint64_t colkey = 0, best = kInf;
                     if (e < n_edges) {
                         const int i = s.edges[e] >> 8, j = s.edges[e] & 255;
-                        is_col = !((s.tree[i] >> j) & 1ull);
-                        if (is_col) {
+                        if (!((s.tree[i] >> j) & 1ull)) {
                             birth = s.D[i][j];
                             colkey = make_key(birth, pack2(i, j));
-                            uint64_t cand = s.adj[i] & s.adj[j];
+                            const uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
-                                uint64_t best = kInf;
-                                int kb = -1;
-                                while (cand) {
-                                    const int k = __ffsll((unsigned long long)cand) - 1;
-                                    cand &= cand - 1;
-                                    const uint64_t key = make_key(fmaxf(birth, fmaxf(s.D[i][k], s.D[j][k])), tri_with(i, j, k));
-                                    if (key < best) { best = key; kb = k; }
-                                }
+                                best = cx.min_cofacet_lane(1, i, j, 0, birth, cand);
                                 death = key_diam(best);
-                                // apparent iff (i,j) is the F-max facet of {i,j,kb}
-                                const uint64_t f1 = cx.ekey(i, kb), f2 = cx.ekey(j, kb);
-                                apparent = colkey > f1 && colkey > f2;
+                                bool col_unused;
+                                // apparent iff (i,j) is the F-max facet of its pivot triangle
+                                apparent = cx.max_facet(1, best, col_unused) == pack2(i, j);
                                 if (apparent) {
                                     const uint32_t tp = key_packed(best);
                                     cx.set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
@@ -628,15 +760,27 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
-                        if (slot < kNACap) cx.na_list()[slot] = colkey;
+                        if (slot < kNACap) {
+                            na_key[slot] = colkey;
+                            na_tau[slot] = best;
+                        }
                     }
                     nna += __popcll(bal);
                 }
                 __syncthreads();
+                DGN_PHASE(2);
+#ifdef DGN_PHASE_TIMING
+                ph[8] += nna;
+                const int a0 = cx.n_adds;
+#endif
                 cx.reduce_serial(1, nna);
-                __syncthreads();
+                lds_sync();
+                DGN_PHASE(3);
+#ifdef DGN_PHASE_TIMING
+                ph[10] += cx.n_adds - a0;
+#endif
             }
-            // ---- dim 2 ----
+            // ---- dim 2: one lane per column (uncleared triangle) ----
             if (dim_max >= 2 && cx.err == 0) {
                 int nna = 0;
                 // stream triangles: each lane owns an edge (a > b) and walks c < b in adj[a] & adj[b]
@@ -644,8 +788,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 int ea = 0, eb = 0;
                 uint64_t tmask = 0;
                 while (true) {
-                    // refill lanes with empty masks
-                    while (true) {
+                    while (true) {  // refill lanes with empty masks
                         const bool need = tmask == 0;
                         const uint64_t bal = ballot(need);
                         if (!bal || next_edge >= n_edges) break;
@@ -662,7 +805,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     if (!ballot(active)) break;
                     bool apparent = false, na_col = false;
                     float birth = 0.f, death = 0.f;
-                    uint64_t colkey = 0;
+                    uint64_t colkey = 0, best = kInf;
                     if (active) {
                         const int a = ea, b = eb;
                         const int c = __ffsll((unsigned long long)tmask) - 1;
@@ -670,26 +813,13 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                         if (!cx.is_cleared(a, b, c)) {
                             birth = cx.tri_diam(a, b, c);
                             colkey = make_key(birth, pack3(a, b, c));
-                            uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
+                            const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
                             if (cand) {
-                                uint64_t best = kInf;
-                                int kb = -1;
-                                while (cand) {
-                                    const int k = __ffsll((unsigned long long)cand) - 1;
-                                    cand &= cand - 1;
-                                    const float dd = fmaxf(birth, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k]));
-                                    const uint64_t key = make_key(dd, tet_with(a, b, c, k));
-                                    if (key < best) { best = key; kb = k; }
-                                }
+                                best = cx.min_cofacet_lane(2, a, b, c, birth, cand);
                                 death = key_diam(best);
-                                // facets containing kb
-                                const uint32_t tp = key_packed(best);
-                                const int p = (tp >> 24) & 255, q = (tp >> 16) & 255, r = (tp >> 8) & 255, t = tp & 255;
-                                uint64_t fm = cx.tkey(p, q, r);
-                                uint64_t k2 = cx.tkey(p, q, t); fm = k2 > fm ? k2 : fm;
-                                k2 = cx.tkey(p, r, t); fm = k2 > fm ? k2 : fm;
-                                k2 = cx.tkey(q, r, t); fm = k2 > fm ? k2 : fm;
-                                apparent = fm == colkey;
+                                bool col_unused;
+                                // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
+                                apparent = cx.max_facet(2, best, col_unused) == pack3(a, b, c);
                                 na_col = !apparent;
                             }
                         }
@@ -698,13 +828,27 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
-                        if (slot < kNACap) cx.na_list()[slot] = colkey;
+                        if (slot < kNACap) {
+                            na_key[slot] = colkey;
+                            na_tau[slot] = best;
+                        }
                     }
                     nna += __popcll(bal);
                 }
                 __syncthreads();
+                DGN_PHASE(4);
+#ifdef DGN_PHASE_TIMING
+                ph[9] += nna;
+                const int a0 = cx.n_adds;
+#endif
                 cx.reduce_serial(2, nna);
-                __syncthreads();
+                lds_sync();
+                DGN_PHASE(5);
+#ifdef DGN_PHASE_TIMING
+                ph[11] += cx.n_adds - a0;
+                ph[12] += cx.n_spills;
+                ph[13] += 1;
+#endif
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
@@ -753,10 +897,10 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     }
                     ss = wave_sum(ss);
                     st[0] = mean;
-                    st[1] = sqrt(ss / (double)m);
+                    st[1] = sqrt(ss / (double)m);  // population std (math.hpp:13-16)
                     st[2] = mx;
                     st[3] = mn;
-                    st[4] = sum * weight;
+                    st[4] = sum * weight;  // weighted_sum = sum * weight (math.hpp:26-28)
                 }
                 const int r = lane - 5 * g;
                 if (r == 0) myval = st[0];
@@ -778,9 +922,14 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 bl.counts[4 * gi + 2] = cx.n_p1;
                 bl.counts[4 * gi + 3] = cx.n_p2;
             }
-            __syncthreads();
+            lds_sync();
+            DGN_PHASE(6);
         }
     }
+#ifdef DGN_PHASE_TIMING
+    if (lane == 0 && bl.phase_cycles)
+        for (int k = 0; k < 16; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -792,7 +941,7 @@ static int np_for(int max_points) { return max_points <= 32 ? 32 : (max_points <
 int betti_grid_waves(int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 1024;
-    // occupancy of the largest instantiation bounds the slots we allocate scratch for
+    // occupancy of the smallest instantiation bounds the slots we allocate scratch for
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<32>, kWave, 0) != hipSuccess || per_cu <= 0)
         per_cu = 8;

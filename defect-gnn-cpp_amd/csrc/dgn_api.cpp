@@ -57,6 +57,7 @@ struct PendingEvent {
 
 struct Scalars {  // device-side scalars, one allocation
     int64_t total;
+    unsigned long long sum_sq;  // sum over atoms of (candidates + 1)^2
     uint32_t max_candidates;
     uint32_t error_flag;
     uint32_t work_counter;
@@ -81,11 +82,16 @@ struct dgn_ctx {
     uint64_t cnt_k = 0;
     uint32_t cnt_max_candidates = 0;
     int64_t cnt_edges = 0;
+    double cnt_sum_sq = 0;
     // betti workspace
     DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch;
     int betti_slots = 0;
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
+#ifdef DGN_PHASE_TIMING
+    DevBuf phase;
+    unsigned long long phase_host[16] = {0};
+#endif
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -191,7 +197,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     {
         TimedLaunch t(c, "graph_count", (double)A * (24 + 4), 0);
         HIP_TRY(c, launch_graph_count(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
-                                      &sc->max_candidates));
+                                      &sc->max_candidates, &sc->sum_sq));
     }
     {
         TimedLaunch t(c, "block_scan", (double)nblocks * 16, 0);
@@ -208,6 +214,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     c->cnt_k = kmax;
     c->cnt_max_candidates = c->host_scalars->max_candidates;
     c->cnt_edges = c->host_scalars->total;
+    c->cnt_sum_sq = (double)c->host_scalars->sum_sq;
     if (num_edges) *num_edges = c->cnt_edges;
     return DGN_OK;
 }
@@ -247,11 +254,13 @@ int check_emit_flag(dgn_ctx* c) {
 }
 
 int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int32_t* counts, const double* clouds,
-               const int32_t* npoints, int32_t cloud_stride, int64_t num_clouds, float* pairs_out, int32_t pair_cap) {
-    const int64_t A = clouds ? num_clouds : b->num_atoms;
+               const int32_t* npoints, int32_t cloud_stride, int64_t num_clouds, float* pairs_out, int32_t pair_cap,
+               const float* lower = nullptr) {
+    const bool given = clouds || lower;
+    const int64_t A = given ? num_clouds : b->num_atoms;
     if (A == 0) return DGN_OK;
     int max_points = cloud_stride;
-    if (!clouds) {
+    if (!given) {
         int64_t E = 0;
         int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E);
         if (st) return st;
@@ -278,12 +287,12 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 2 * sizeof(uint32_t), c->stream));
     BettiLaunch bl{};
-    bl.row_ptr = clouds ? nullptr : c->b_row_ptr.as<int64_t>();
-    bl.disp = clouds ? nullptr : c->b_disp.as<double>();
-    bl.pos = clouds ? nullptr : b->positions;
-    bl.species = clouds ? nullptr : b->species;
-    bl.atom_offset = clouds ? nullptr : b->atom_offset;
-    bl.num_structures = clouds ? 0 : b->num_structures;
+    bl.row_ptr = given ? nullptr : c->b_row_ptr.as<int64_t>();
+    bl.disp = given ? nullptr : c->b_disp.as<double>();
+    bl.pos = given ? nullptr : b->positions;
+    bl.species = given ? nullptr : b->species;
+    bl.atom_offset = given ? nullptr : b->atom_offset;
+    bl.num_structures = given ? 0 : b->num_structures;
     bl.num_atoms = A;
     bl.thr = (float)rc;  // ripser_wrapper.cpp:28
     bl.features = features;
@@ -293,20 +302,30 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.scratch = c->b_scratch.as<uint8_t>();
     bl.scratch_per_wave = spw;
     bl.clouds = clouds;
+    bl.lower = lower;
     bl.npoints = npoints;
     bl.cloud_stride = cloud_stride;
     bl.pairs_out = pairs_out;
     bl.pair_cap = pair_cap;
+#ifdef DGN_PHASE_TIMING
+    HIP_TRY(c, c->phase.ensure(16 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 16 * sizeof(unsigned long long), c->stream));
+    bl.phase_cycles = c->phase.as<unsigned long long>();
+#endif
     {
         // algorithmic bytes: CSR rows in (disp 24 B/edge + row_ptr) + positions + 35 f64 + 4 i32 out;
         // flops: 6 n^2 per complex for the Gram product is accounted in DESIGN.md, not here
-        const double bytes = clouds ? 0.0 : ((double)c->cnt_edges * 24 + (double)A * (8 + 24 + 4 + 35 * 8 + 16));
-        TimedLaunch t(c, "betti_vr", bytes, 0);
+        const double bytes = given ? 0.0 : ((double)c->cnt_edges * 24 + (double)A * (8 + 24 + 4 + 35 * 8 + 16));
+        // useful flops of the local Gram product: 6 n^2 per complex
+        TimedLaunch t(c, "betti_vr", bytes, given ? 0.0 : 6.0 * c->cnt_sum_sq);
         HIP_TRY(c, launch_betti(c->stream, bl, max_points, c->betti_slots));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
                               c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+#ifdef DGN_PHASE_TIMING
+    HIP_TRY(c, hipMemcpy(c->phase_host, c->phase.p, sizeof(c->phase_host), hipMemcpyDeviceToHost));
+#endif
     const uint32_t f = c->host_scalars->error_flag;
     if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
     if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
@@ -579,23 +598,26 @@ int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, do
     return st;
 }
 
-int dgn_host_persistence(dgn_ctx* c, const double* clouds, const int32_t* npoints, int64_t C, int32_t max_points,
-                         double threshold, float* pairs, int32_t cap, int32_t* counts) {
-    if (!c || !clouds || !npoints || C < 0 || max_points <= 0 || cap <= 0)
+static int host_persistence_common(dgn_ctx* c, const double* clouds, const float* lower, const int32_t* npoints,
+                                   int64_t C, int32_t max_points, double threshold, float* pairs, int32_t cap,
+                                   int32_t* counts) {
+    if (!c || (!clouds && !lower) || !npoints || C < 0 || max_points <= 0 || cap <= 0 || !pairs)
         return fail(c, DGN_ERR_ARG, "dgn_host_persistence: bad args");
     if (C == 0) return DGN_OK;
     for (int64_t i = 0; i < C; ++i)
         if (npoints[i] < 1 || npoints[i] > max_points) return fail(c, DGN_ERR_ARG, "npoints out of range");
     HIP_TRY(c, hipSetDevice(c->device));
     DevBuf dc, dn, dp, dk;
+    const size_t in_bytes = clouds ? 24 * (size_t)C * max_points
+                                   : 4 * (size_t)C * ((size_t)max_points * (max_points - 1) / 2);
     hipError_t e;
-    if ((e = dc.ensure(24 * (size_t)C * max_points)) || (e = dn.ensure(4 * (size_t)C)) ||
-        (e = dp.ensure(8 * 3 * (size_t)C * cap)) || (e = dk.ensure(16 * (size_t)C)))
+    if ((e = dc.ensure(in_bytes)) || (e = dn.ensure(4 * (size_t)C)) || (e = dp.ensure(8 * 3 * (size_t)C * cap)) ||
+        (e = dk.ensure(16 * (size_t)C)))
         return hip_fail(c, e, "dgn_host_persistence: allocation");
-    HIP_TRY(c, hipMemcpy(dc.p, clouds, 24 * (size_t)C * max_points, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(dc.p, clouds ? (const void*)clouds : (const void*)lower, in_bytes, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dn.p, npoints, 4 * (size_t)C, hipMemcpyHostToDevice));
-    int st = betti_impl(c, nullptr, threshold, nullptr, dk.as<int32_t>(), dc.as<double>(), dn.as<int32_t>(), max_points,
-                        C, dp.as<float>(), cap);
+    int st = betti_impl(c, nullptr, threshold, nullptr, dk.as<int32_t>(), clouds ? dc.as<double>() : nullptr,
+                        dn.as<int32_t>(), max_points, C, dp.as<float>(), cap, clouds ? nullptr : dc.as<float>());
     std::vector<int32_t> kk(4 * C);
     if (!st) {
         HIP_TRY(c, hipMemcpy(kk.data(), dk.p, 16 * (size_t)C, hipMemcpyDeviceToHost));
@@ -618,6 +640,57 @@ int dgn_host_persistence(dgn_ctx* c, const double* clouds, const int32_t* npoint
     dk.release();
     return st;
 }
+
+int dgn_host_persistence(dgn_ctx* c, const double* clouds, const int32_t* npoints, int64_t C, int32_t max_points,
+                         double threshold, float* pairs, int32_t cap, int32_t* counts) {
+    if (!clouds) return fail(c, DGN_ERR_ARG, "dgn_host_persistence: null clouds");
+    return host_persistence_common(c, clouds, nullptr, npoints, C, max_points, threshold, pairs, cap, counts);
+}
+
+int dgn_host_persistence_lower(dgn_ctx* c, const float* lower, const int32_t* npoints, int64_t C, int32_t max_points,
+                               double threshold, float* pairs, int32_t cap, int32_t* counts) {
+    if (!lower) return fail(c, DGN_ERR_ARG, "dgn_host_persistence_lower: null matrix");
+    return host_persistence_common(c, nullptr, lower, npoints, C, max_points, threshold, pairs, cap, counts);
+}
+
+int dgn_host_rbf(dgn_ctx* c, const double* distances, int64_t E, double rbf_cutoff, double rbf_dr, int32_t dtype,
+                 int32_t layout, void* out) {
+    if (!c || E < 0 || (E && (!distances || !out)) || (dtype != DGN_F32 && dtype != DGN_F64) ||
+        (layout != 0 && layout != 1) || !(rbf_dr > 0) || dgn_rbf_bins(rbf_cutoff, rbf_dr) <= 0)
+        return fail(c, DGN_ERR_ARG, "dgn_host_rbf: bad args");
+    if (E == 0) return DGN_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    dgn_graph_params p;
+    dgn_graph_params_default(&p);
+    p.rbf_cutoff = rbf_cutoff;
+    p.rbf_dr = rbf_dr;
+    p.rbf_dtype = dtype;
+    const RbfSpec rs = make_rbf(&p);
+    const size_t elem = dtype == DGN_F32 ? 4 : 8;
+    DevBuf dd, dout;
+    hipError_t e;
+    if ((e = dd.ensure(8 * (size_t)E)) || (e = dout.ensure(elem * (size_t)E * rs.nbins)))
+        return hip_fail(c, e, "dgn_host_rbf: allocation");
+    HIP_TRY(c, hipMemcpyAsync(dd.p, distances, 8 * (size_t)E, hipMemcpyHostToDevice, c->stream));
+    {
+        TimedLaunch t(c, "rbf", (double)E * 8 + (double)E * rs.nbins * elem, 0);
+        HIP_TRY(c, launch_rbf(c->stream, dd.as<double>(), E, rs, layout, dout.p));
+    }
+    HIP_TRY(c, hipMemcpyAsync(out, dout.p, elem * (size_t)E * rs.nbins, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    dd.release();
+    dout.release();
+    return DGN_OK;
+}
+
+#ifdef DGN_PHASE_TIMING
+/* diagnostics build only (libdgn_diag.so): per-phase s_memtime cycles of the last Betti launch */
+int dgn_diag_phase_cycles(dgn_ctx* c, unsigned long long* out) {
+    if (!c || !out) return DGN_ERR_ARG;
+    std::memcpy(out, c->phase_host, sizeof(c->phase_host));
+    return DGN_OK;
+}
+#endif
 
 int64_t dgn_synth_atoms_per_structure(int kind, int m) {
     if (m <= 0) return -1;

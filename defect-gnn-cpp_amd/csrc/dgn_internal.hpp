@@ -30,12 +30,14 @@ struct RbfSpec {
 hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset,
                                   int64_t num_structures, double rc, StructMeta* meta);
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint32_t* max_candidates);
+                              uint32_t* max_candidates, unsigned long long* sum_sq);
 hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, int64_t nblocks, int64_t* total);
 // cap: candidate capacity per query atom (>= max candidates from the count pass)
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag);
+
+hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out);
 
 inline int64_t graph_blocks(int64_t num_atoms) { return (num_atoms + kAtomsPerBlock - 1) / kAtomsPerBlock; }
 int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
@@ -57,11 +59,14 @@ struct BettiLaunch {
     int64_t scratch_per_wave;
     // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
     const double* clouds;
+    // optional distance-input mode (dgn_host_persistence_lower): lower[c][stride*(stride-1)/2] f32
+    const float* lower;
     const int32_t* npoints;
     int32_t cloud_stride;     // max_points
     // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
     float* pairs_out;
     int32_t pair_cap;
+    unsigned long long* phase_cycles;  // [16] diagnostics build only (DGN_PHASE_TIMING)
 };
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();

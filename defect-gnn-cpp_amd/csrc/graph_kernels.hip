@@ -141,12 +141,14 @@ __device__ __forceinline__ uint64_t pack_jimg(int j, int na, int nb, int nc) {
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
                                                                    int64_t* __restrict__ block_sums,
-                                                                   uint32_t* __restrict__ max_candidates) {
+                                                                   uint32_t* __restrict__ max_candidates,
+                                                                   unsigned long long* __restrict__ sum_sq) {
     __shared__ int64_t wsum[kGraphBlock / kWave];
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
     int64_t my_sum = 0;
     uint32_t my_max = 0;
+    unsigned long long my_sq = 0;
     for (int t = w; t < kAtomsPerBlock; t += kGraphBlock / kWave) {
         const int64_t gi = (int64_t)blockIdx.x * kAtomsPerBlock + t;
         if (gi >= g.num_atoms) break;
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g,
         if (lane == 0) counts[gi] = (int32_t)c;
         my_sum += c;
         my_max = (uint32_t)m > my_max ? (uint32_t)m : my_max;
+        my_sq += (unsigned long long)(m + 1) * (unsigned long long)(m + 1);  // local-complex n^2
     }
     if (lane == 0) wsum[w] = my_sum;
     __syncthreads();
@@ -169,6 +172,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g,
         block_sums[blockIdx.x] = s;
     }
     if (lane == 0 && my_max) atomicMax(max_candidates, my_max);
+    if (lane == 0 && my_sq) atomicAdd(sum_sq, my_sq);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -326,6 +330,37 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 }
 
 // ------------------------------------------------------------------------------------------
+// RBF of caller-given distances (CrystalGraph edge_attr), flat over the output so stores are
+// coalesced in either layout: layout 0 row-major [E][nb], layout 1 column-major (k*E + e).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rbf_kernel(const double* __restrict__ d, int64_t E, RbfSpec rs, int layout,
+                                                  void* __restrict__ out) {
+    const int64_t total = E * rs.nbins;
+    for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < total; f += (int64_t)gridDim.x * blockDim.x) {
+        int64_t e;
+        int k;
+        if (layout == 0) {
+            e = f / rs.nbins;
+            k = (int)(f - e * rs.nbins);
+        } else {
+            k = (int)(f / E);
+            e = f - (int64_t)k * E;
+        }
+        if (rs.dtype == 1) reinterpret_cast<float*>(out)[f] = rbf_value_f32(d[e], k, rs);
+        else reinterpret_cast<double*>(out)[f] = rbf_value_f64(d[e], k, rs);
+    }
+}
+
+hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out) {
+    const int64_t total = E * rs.nbins;
+    if (total <= 0) return hipSuccess;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(rbf_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d, E, rs, layout, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
 hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset, int64_t B,
@@ -338,11 +373,11 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
 }
 
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint32_t* max_candidates) {
+                              uint32_t* max_candidates, unsigned long long* sum_sq) {
     const int64_t nb = graph_blocks(g.num_atoms);
     if (nb <= 0) return hipSuccess;
     hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
-                       max_candidates);
+                       max_candidates, sum_sq);
     return hipGetLastError();
 }
 

@@ -8,7 +8,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(os.path.dirname(HERE))  # defect-gnn-cpp_amd/
-lib_path = os.path.join(PKG, "lib", "libdgn.so")
+lib_path = os.environ.get("DGN_LIB") or os.path.join(PKG, "lib", "libdgn.so")
 
 DGN_NONE, DGN_F32, DGN_F64 = 0, 1, 2
 STATUS = {0: "DGN_OK", 1: "DGN_ERR_ARG", 2: "DGN_ERR_HIP", 3: "DGN_ERR_CAPACITY", 4: "DGN_ERR_NODEVICE",
@@ -21,6 +21,7 @@ EXPORTS = [
     "dgn_ctx_last_error", "dgn_ctx_enable_timing", "dgn_ctx_kernel_times", "dgn_ctx_reset_timing",
     "dgn_graph_params_default", "dgn_rbf_bins", "dgn_dev_graph_count", "dgn_dev_graph_emit", "dgn_host_graph",
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
+    "dgn_host_persistence_lower", "dgn_host_rbf",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch",
 ]
 
@@ -97,6 +98,8 @@ def lib():
     L.dgn_dev_betti.argtypes = [vp, C.POINTER(Batch), C.POINTER(BettiParams), vp, vp]
     L.dgn_host_betti.argtypes = [vp, C.POINTER(Batch), C.POINTER(BettiParams), vp, vp]
     L.dgn_host_persistence.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
+    L.dgn_host_persistence_lower.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
+    L.dgn_host_rbf.argtypes = [vp, vp, i64, dbl, dbl, i32, i32, vp]
     L.dgn_synth_atoms_per_structure.restype = i64
     L.dgn_synth_atoms_per_structure.argtypes = [C.c_int, C.c_int]
     L.dgn_synth_batch.argtypes = [C.c_int, C.c_int, i64, i64, vp, vp, vp, vp]
@@ -232,6 +235,25 @@ class Context:
         self._check(lib().dgn_host_persistence(self.h, _ptr(clouds), _ptr(npoints), Cn, maxp, threshold,
                                                _ptr(pairs), cap, _ptr(counts)), "dgn_host_persistence")
         return pairs, counts
+
+    def host_persistence_lower(self, lower, npoints, max_points: int, threshold: float, cap: int = 512):
+        lower = np.ascontiguousarray(lower, dtype=np.float32)
+        npoints = np.ascontiguousarray(npoints, dtype=np.int32)
+        Cn = npoints.shape[0]
+        assert lower.shape == (Cn, max_points * (max_points - 1) // 2)
+        pairs = np.zeros((Cn, 3, cap, 2), np.float32)
+        counts = np.zeros((Cn, 4), np.int32)
+        self._check(lib().dgn_host_persistence_lower(self.h, _ptr(lower), _ptr(npoints), Cn, max_points, threshold,
+                                                     _ptr(pairs), cap, _ptr(counts)), "dgn_host_persistence_lower")
+        return pairs, counts
+
+    def host_rbf(self, distances, rbf_cutoff=10.0, rbf_dr=0.1, dtype=DGN_F64, layout=0):
+        d = np.ascontiguousarray(distances, dtype=np.float64)
+        nb = lib().dgn_rbf_bins(rbf_cutoff, rbf_dr)
+        out = np.zeros(d.shape[0] * nb, np.float32 if dtype == DGN_F32 else np.float64)
+        self._check(lib().dgn_host_rbf(self.h, _ptr(d), d.shape[0], rbf_cutoff, rbf_dr, dtype, layout, _ptr(out)),
+                    "dgn_host_rbf")
+        return out.reshape(d.shape[0], nb) if layout == 0 else out.reshape(nb, d.shape[0]).T
 
     # ---- device-level API (torch tensors on cuda) ----
     def dev_graph_count(self, batch: dict, params: GraphParams) -> int:

@@ -152,6 +152,20 @@ int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_pa
 int dgn_host_persistence(dgn_ctx* ctx, const double* clouds, const int32_t* npoints, int64_t num_clouds,
                          int32_t max_points, double threshold, float* pairs, int32_t cap, int32_t* counts);
 
+/* Gaussian RBF of caller-given distances (replaces the per-edge gaussian_rbf calls of
+ * CrystalGraph, src/graph/crystal_graph.cpp:32-40). Host arrays. layout 0 = row-major [E][n_rbf],
+ * 1 = column-major (Eigen MatrixXd edge_attr: element (e,k) at k*E + e). dtype DGN_F32/DGN_F64. */
+int dgn_host_rbf(dgn_ctx* ctx, const double* distances, int64_t num_edges, double rbf_cutoff,
+                 double rbf_dr, int32_t dtype, int32_t layout, void* out);
+
+/* Persistence from caller-given distance matrices (replaces
+ * topology::compute_persistence_from_distances, src/topology/ripser_wrapper.cpp:11-58): lower:
+ * [C][max_points*(max_points-1)/2] f32, the strict lower triangle row by row (i = 1..n-1, j < i)
+ * exactly as ripser_wrapper.cpp:20-24 packs it; other arguments as dgn_host_persistence. */
+int dgn_host_persistence_lower(dgn_ctx* ctx, const float* lower, const int32_t* npoints, int64_t num_clouds,
+                               int32_t max_points, double threshold, float* pairs, int32_t cap,
+                               int32_t* counts);
+
 /* ---- synthetic batches (bench/test inputs) -----------------------
  * kind 0 = simple cubic m^3 (s = 2.32 A), kind 1 = FCC m^3 cells (a = 3.684 A). Host arrays:
  * lattice [B][9], positions [B*n][3], species [B*n], atom_offset [B+1]. */

@@ -409,6 +409,25 @@ int64_t oracle_neighbor_list(const double* L, const double* pos, int64_t n, doub
 
 int oracle_rbf_bins(double rc, double dr) { return (int)std::floor(rc / dr); }
 
+int64_t oracle_structure_graph(const double* L, const double* pos, int64_t n, double rc, uint64_t kmax, double eps,
+                               double rbf_rc, double dr, double* rbf_out) {
+    // CrystalGraph edge part (crystal_graph.cpp:23-40): NeighborList rows, one gaussian_rbf per edge
+    std::vector<std::vector<Candidate>> rows;
+    neighbor_rows(L, pos, n, rc, kmax, eps, rows);
+    const int nb = oracle_rbf_bins(rbf_rc, dr);
+    std::vector<double> g(nb);
+    int64_t e = 0;
+    double sink = 0;
+    for (int64_t i = 0; i < n; ++i)
+        for (const Candidate& c : rows[i]) {
+            oracle_gaussian_rbf(c.distance, rbf_rc, dr, rbf_out ? rbf_out + e * nb : g.data());
+            sink += g[0];
+            ++e;
+        }
+    if (sink == -1.0) e = -1;  // keep the work observable
+    return e;
+}
+
 void oracle_gaussian_rbf(double distance, double rc, double dr, double* g) {
     // edge_features.cpp:7-24, same operation sequence
     int n = std::floor(rc / dr);

@@ -44,6 +44,12 @@ int oracle_num_images(const double* lattice, double r_cutoff);
 int oracle_rbf_bins(double r_cutoff, double dr);
 void oracle_gaussian_rbf(double distance, double r_cutoff, double dr, double* out);
 
+/* CrystalGraph edge part for one structure (neighbour rows + one RBF per edge); rbf_out may be
+ * NULL (timing only). Returns E. */
+int64_t oracle_structure_graph(const double* lattice, const double* pos, int64_t n, double r_cutoff,
+                               uint64_t max_neighbors, double epsilon, double rbf_cutoff, double dr,
+                               double* rbf_out);
+
 /* ---- local distance matrix (ripser_wrapper.cpp:60-70 then :17-24) --------------------- */
 /* cloud [n][3] f64 -> strict lower triangle, row i=1..n-1, j<i, as float32. */
 void oracle_local_distances(const double* cloud, int n, float* lower);

@@ -38,6 +38,10 @@ def lib():
         _lib.oracle_num_images.argtypes = [C.POINTER(C.c_double), C.c_double]
         _lib.oracle_rbf_bins.restype = C.c_int
         _lib.oracle_rbf_bins.argtypes = [C.c_double, C.c_double]
+        _lib.oracle_structure_graph.restype = C.c_int64
+        _lib.oracle_structure_graph.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int64, C.c_double,
+                                                C.c_uint64, C.c_double, C.c_double, C.c_double,
+                                                C.POINTER(C.c_double)]
         _lib.oracle_gaussian_rbf.argtypes = [C.c_double, C.c_double, C.c_double, C.POINTER(C.c_double)]
         _lib.oracle_local_distances.argtypes = [C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_float)]
         _lib.oracle_persistence.restype = C.c_int
@@ -164,3 +168,18 @@ def ref_structure_betti(lattice, pos, species, r_cutoff, omp_threads=8, ripser_t
     ref().ref_structure_betti(_p(L, C.c_double), _p(P, C.c_double), _p(S, C.c_int32), n, r_cutoff,
                               omp_threads, ripser_threads, _p(f, C.c_double), _p(c, C.c_int32))
     return f, c
+
+
+def structure_graph(lattice, pos, r_cutoff, max_neighbors, rbf_cutoff, dr, want_rbf=False):
+    L = np.ascontiguousarray(lattice, dtype=np.float64)
+    P = np.ascontiguousarray(pos, dtype=np.float64)
+    k = (1 << 64) - 1 if max_neighbors is None else int(max_neighbors)
+    if not want_rbf:
+        return lib().oracle_structure_graph(_p(L, C.c_double), _p(P, C.c_double), P.shape[0], r_cutoff, k, 1e-10,
+                                            rbf_cutoff, dr, None)
+    e = lib().oracle_structure_graph(_p(L, C.c_double), _p(P, C.c_double), P.shape[0], r_cutoff, k, 1e-10,
+                                     rbf_cutoff, dr, None)
+    out = np.zeros((e, lib().oracle_rbf_bins(rbf_cutoff, dr)))
+    lib().oracle_structure_graph(_p(L, C.c_double), _p(P, C.c_double), P.shape[0], r_cutoff, k, 1e-10, rbf_cutoff,
+                                 dr, _p(out, C.c_double))
+    return out

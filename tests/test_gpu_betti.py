@@ -91,3 +91,23 @@ def test_isolated_atom(ctx):
     f, c = ctx.host_betti(one, 5.0)
     assert np.all(f == 0.0)
     assert c.tolist() == [[0, 1, 0, 0], [0, 1, 0, 0]]
+
+
+def test_persistence_from_distance_matrix(ctx):
+    # compute_persistence_from_distances input mode: the packed f32 lower triangle
+    rng = np.random.default_rng(9)
+    maxp, C = 40, 50
+    npts = rng.integers(2, maxp + 1, size=C).astype(np.int32)
+    lows = np.zeros((C, maxp * (maxp - 1) // 2), np.float32)
+    refs = []
+    for c in range(C):
+        pts = rng.uniform(0, 4, size=(npts[c], 3))
+        low = O.local_distances(pts)
+        lows[c, :low.shape[0]] = low
+        refs.append(O.persistence(low, npts[c], np.float32(2.5)))
+    # the kernel reads row i at offset i*(i-1)/2 of a max_points-sized triangle: same packing
+    pairs, counts = ctx.host_persistence_lower(lows, npts, maxp, 2.5, cap=256)
+    for c in range(C):
+        r = refs[c]
+        assert np.array_equal(pairs[c, 1, :counts[c, 2]], r["dim1"]) and np.array_equal(pairs[c, 2, :counts[c, 3]], r["dim2"])
+        assert np.array_equal(pairs[c, 0, :counts[c, 0]], r["dim0"])

@@ -109,3 +109,13 @@ def test_empty_and_ragged(ctx):
     assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
     lone_row = sizes[0]
     assert rp[lone_row + 1] - rp[lone_row] == 0
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+def test_rbf_of_given_distances(ctx, layout):
+    d = np.linspace(0.0, 9.99, 777)
+    for dt, tol in ((dgn.DGN_F64, 1e-13), (dgn.DGN_F32, RBF_RTOL)):
+        out = ctx.host_rbf(d, 10.0, 0.1, dt, layout)
+        ref = np.stack([O.gaussian_rbf(x, 10.0, 0.1) for x in d])
+        assert out.shape == ref.shape
+        assert np.max(np.abs(out - ref) / ref) < tol

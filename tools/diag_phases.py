@@ -1,0 +1,38 @@
+"""Diagnostics: per-phase cycle breakdown of the Betti kernel (libdgn_diag.so, s_memtime stamps).
+Usage: DGN_LIB=defect-gnn-cpp_amd/lib/libdgn_diag.so python tools/diag_phases.py [kind] [m] [B] [rc]"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("DGN_LIB", os.path.join(ROOT, "defect-gnn-cpp_amd", "lib", "libdgn_diag.so"))
+sys.path[:0] = [os.path.join(ROOT, "defect-gnn-cpp_amd", "python")]
+import numpy as np  # noqa: E402
+
+import dgn  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else "fcc"
+m = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+B = int(sys.argv[3]) if len(sys.argv) > 3 else 512
+rc = float(sys.argv[4]) if len(sys.argv) > 4 else 5.0
+ctx = dgn.Context(0)
+batch = dgn.synth_batch(kind, m, B)
+A = batch["positions"].shape[0]
+ctx.host_betti(batch, rc)  # warm-up
+t0 = time.perf_counter()
+f, c = ctx.host_betti(batch, rc)
+dt = time.perf_counter() - t0
+ph = (C.c_ulonglong * 16)()
+dgn.lib().dgn_diag_phase_cycles(ctx.h, ph)
+ph = list(ph)
+names = ["load+gram", "adj+prim+edges", "dim1 apparent", "dim1 serial", "dim2 apparent", "dim2 serial",
+         "stats+write", "dequeue/gap"]
+tot = sum(ph[:8])
+out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round(dt, 4),
+       "cycles_per_complex": round(tot / A), "phase_cycles_per_complex": {n: round(ph[i] / A) for i, n in enumerate(names)},
+       "phase_share": {n: round(ph[i] / tot, 4) for i, n in enumerate(names)},
+       "na1_per_complex": ph[8] / A, "na2_per_complex": ph[9] / A, "adds1": ph[10] / A, "adds2": ph[11] / A,
+       "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13]}
+print(json.dumps(out, indent=1))
