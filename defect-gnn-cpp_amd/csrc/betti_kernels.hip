@@ -32,11 +32,12 @@
 
 namespace dgn {
 
-constexpr int kVCap = 256;        // simplices in one column's V list
-constexpr int kVStoreLds = 512;   // stored V-list entries kept in LDS (rest in scratch)
+constexpr int kVCap = 128;        // simplices in one column's V list (LDS)
+constexpr int kVStoreLds = 128;   // stored V-list entries kept in LDS (rest in scratch)
+constexpr int kNALds = 64;        // sorted non-apparent column records kept in LDS
 constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
 constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
-constexpr int kPivLds = 128;      // serially resolved pivots kept in LDS (rest in scratch)
+constexpr int kPivLds = 64;       // serially resolved pivots kept in LDS (rest in scratch)
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
 constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
 constexpr int kChunk = 4;         // complexes per dequeue
@@ -65,12 +66,15 @@ struct ScratchLayout {
     static constexpr int64_t p1 = piv + 8 * kPivCap;                 // float2 [kPairCap]
     static constexpr int64_t p2 = p1 + 8 * kPairCap;                 // float2 [kPairCap]
     static constexpr int64_t vstore = p2 + 8 * kPairCap;             // uint32 [kVStoreCap]
-    static constexpr int64_t total = vstore + 4 * kVStoreCap;
+    // F-minimal cofacet (packed) of every edge / triangle of the complex, indexed by its dense
+    // combinatorial index; kNone for simplices that are not columns or have no cofacet
+    static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint32 [C(64,3)]
+    static constexpr int64_t total = mincof + 4 * (64 * 63 * 62 / 6);
 };
 
 template <int NP>
 struct BettiSmem {
-    float D[NP][NP + 1];
+    float Dt[NP * (NP - 1) / 2];  // f32 distances, strict lower triangle: (i > j) at i(i-1)/2 + j
     uint64_t adj[NP];
     uint64_t tree[NP];
     uint16_t edges[NP * (NP - 1) / 2];
@@ -81,9 +85,12 @@ struct BettiSmem {
             double X[NP][3];
             double sq[NP];
         } cloud;
-        uint64_t sort_keys[kVStoreLds / 2];
-        uint32_t vstore[kVStoreLds];
+        struct {
+            uint64_t key[kNALds];
+            uint64_t tau[kNALds];
+        } na;
     } u;
+    uint32_t vstore[kVStoreLds];
     uint32_t vcur[kVCap];
     uint64_t piv[kPivLds];
     uint32_t vmeta[kPivLds];
@@ -98,6 +105,23 @@ struct BettiSmem {
 // fence (s_waitcnt vmcnt(0)) that stalls on every in-flight global load/store; it is kept only
 // where data passes between lanes through global scratch.
 __device__ __forceinline__ void lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// move a wave-uniform value to an SGPR so dependent integer math runs on the scalar unit
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+// materialize a value in a VGPR here (stops the compiler from sinking select arms into
+// divergent branches; the arms below are cheap and computed unconditionally)
+__device__ __forceinline__ uint32_t pin(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int pin(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int c2(int x) { return x * (x - 1) / 2; }
+__device__ __forceinline__ int c3(int x) { return x * (x - 1) * (x - 2) / 6; }
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, kWave);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
@@ -178,12 +202,33 @@ struct Complex {
     // pair counts (wave-uniform)
     int n_d0, n_inf0, n_p1, n_p2;
     int n_adds, n_spills;  // diagnostics
+#ifdef DGN_PHASE_TIMING
+    uint64_t* ph = nullptr;
+    uint64_t* tprev = nullptr;
+    __device__ void stamp(int k) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        ph[k] += t - *tprev;
+        *tprev = t;
+    }
+#define DGN_SUB(k) stamp(k)
+#else
+#define DGN_SUB(k) \
+    do {           \
+    } while (0)
+#endif
 
+    __device__ float dlow(int a, int b) const { return s.Dt[c2(a) + b]; }  // a > b
+    __device__ float dist(int i, int j) const {                              // i != j
+        const int a = i > j ? i : j, b = i > j ? j : i;
+        return s.Dt[c2(a) + b];
+    }
     __device__ uint64_t ekey(int i, int j) const {  // i != j
         const int a = i > j ? i : j, b = i > j ? j : i;
-        return make_key(s.D[a][b], pack2(a, b));
+        return make_key(s.Dt[c2(a) + b], pack2(a, b));
     }
-    __device__ float tri_diam(int a, int b, int c) const { return fmaxf(fmaxf(s.D[a][b], s.D[a][c]), s.D[b][c]); }
+    __device__ float tri_diam(int a, int b, int c) const {  // a > b > c
+        return fmaxf(fmaxf(dlow(a, b), dlow(a, c)), dlow(b, c));
+    }
     __device__ uint64_t tkey(int a, int b, int c) const { return make_key(tri_diam(a, b, c), pack3(a, b, c)); }
     __device__ bool is_cleared(int a, int b, int c) const {
         const int t = tri_dense(a, b, c);
@@ -228,8 +273,8 @@ struct Complex {
                 if (u < m) {
                     const int k = ks[u];
                     uint64_t key;
-                    if (dim == 1) key = make_key(fmaxf(diam, fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
-                    else key = make_key(fmaxf(diam, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k])), tet_with(a, b, c, k));
+                    if (dim == 1) key = make_key(fmaxf(diam, fmaxf(dist(a, k), dist(b, k))), tri_with(a, b, k));
+                    else key = make_key(fmaxf(diam, fmaxf(fmaxf(dist(a, k), dist(b, k)), dist(c, k))), tet_with(a, b, c, k));
                     best = key < best ? key : best;
                 }
             }
@@ -242,8 +287,8 @@ struct Complex {
         const int k = lane_id();
         uint64_t key = kInf;
         if ((cand >> k) & 1ull) {
-            if (dim == 1) key = make_key(fmaxf(diam, fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
-            else key = make_key(fmaxf(diam, fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k])), tet_with(a, b, c, k));
+            if (dim == 1) key = make_key(fmaxf(diam, fmaxf(dist(a, k), dist(b, k))), tri_with(a, b, k));
+            else key = make_key(fmaxf(diam, fmaxf(fmaxf(dist(a, k), dist(b, k)), dist(c, k))), tet_with(a, b, c, k));
         }
         return wave_min_u64(key);
     }
@@ -276,19 +321,13 @@ struct Complex {
             return pack3(fa, fb, fc);
         }
     }
+    // Apparent owner of pivot tau (whole wave, uniform): its F-max facet f, if tau is f's
+    // F-minimal cofacet (recorded for every column by the lane-parallel pass), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         bool col;
-        const uint32_t f = max_facet(dim, tau, col);
-        if (!col) return kNone;
-        uint64_t m;
-        if (dim == 1) {
-            const int fa = (f >> 8) & 255, fb = f & 255;
-            m = min_cofacet_wave(1, fa, fb, 0, s.D[fa][fb], s.adj[fa] & s.adj[fb]);
-        } else {
-            const int fa = (f >> 16) & 255, fb = (f >> 8) & 255, fc = f & 255;
-            m = min_cofacet_wave(2, fa, fb, fc, tri_diam(fa, fb, fc), s.adj[fa] & s.adj[fb] & s.adj[fc]);
-        }
-        return m == tau ? f : kNone;
+        const uint32_t f = uni(max_facet(dim, uni64(tau), col));
+        const uint32_t m = sp<uint32_t>(ScratchLayout::mincof)[col_dense(dim, f)];
+        return uni(m) == key_packed(tau) ? f : kNone;
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {
@@ -313,38 +352,61 @@ struct Complex {
     // multiplicity. Cofacet tau = s u {k} is evaluated by lane k for each s in V; its other
     // facets are found in V through the LDS bitmap, and only the packed-smallest facet of tau
     // in V reports it (so each tau is counted once). kInf for the zero column.
-    __device__ uint64_t pivot_of_V(int dim, int v) const {
+    __device__ uint64_t pivot_of_V(int dim, int v_) const {
+        // Branch-free body: every lane evaluates its vertex k for every V entry (uniform terms
+        // on the scalar unit, per-lane arms selected with v_cndmask) and masks at the end.
         const int k = lane_id();
+        const int c2k = c2(k), c3k = c3(k);
+        const int v = (int)uni((uint32_t)v_);
         uint64_t best = kInf;
         for (int i = 0; i < v; ++i) {
-            const uint32_t sp_ = s.vcur[i];
+            const uint32_t sp_ = uni(s.vcur[i]);
             if (dim == 1) {
                 const int a = (sp_ >> 8) & 255, b = sp_ & 255;
-                const uint64_t cand = s.adj[a] & s.adj[b];
-                if ((cand >> k) & 1ull) {
-                    const uint32_t f1 = sort2(a, k), f2 = sort2(b, k);
-                    const bool m1 = vbit(col_dense(1, f1)), m2 = vbit(col_dense(1, f2));
-                    const bool odd = !(m1 ^ m2);  // 1 + m1 + m2 odd
-                    const bool rep = !(m1 && f1 < sp_) && !(m2 && f2 < sp_);
-                    if (odd && rep) {
-                        const uint64_t key = make_key(fmaxf(s.D[a][b], fmaxf(s.D[a][k], s.D[b][k])), tri_with(a, b, k));
-                        best = key < best ? key : best;
-                    }
-                }
+                const uint64_t cand = uni64(s.adj[a]) & uni64(s.adj[b]);
+                const int C2a = c2(a), C2b = c2(b), ds = C2a + b;
+                const float dab = __uint_as_float(uni(__float_as_uint(dlow(a, b))));
+                const bool on = (cand >> k) & 1ull;
+                const bool ga = k > a, gb = k > b;
+                const int t11 = pin(c2k + a), t12 = pin(C2a + k), t21 = pin(c2k + b), t22 = pin(C2b + k);
+                const int d1 = ga ? t11 : t12;  // {a, k}
+                const int d2 = gb ? t21 : t22;  // {b, k}
+                const bool m1 = vbit(on ? d1 : 0), m2 = vbit(on ? d2 : 0);
+                const bool odd = !(m1 ^ m2);  // 1 + m1 + m2 odd
+                const bool rep = !(m1 && d1 < ds) && !(m2 && d2 < ds);
+                // edge {a,k} / {b,k} indices are d1 / d2 (clamped for idle lanes)
+                const float dd = fmaxf(dab, fmaxf(s.Dt[on ? d1 : 0], s.Dt[on ? d2 : 0]));
+                const uint32_t p1 = pin(pack3(k, a, b)), p2 = pin(pack3(a, k, b)), p3 = pin(pack3(a, b, k));
+                const uint32_t pk = ga ? p1 : (gb ? p2 : p3);
+                const uint64_t key = make_key(dd, pk);
+                best = (on && odd && rep && key < best) ? key : best;
             } else {
                 const int a = (sp_ >> 16) & 255, b = (sp_ >> 8) & 255, c = sp_ & 255;
-                const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
-                if ((cand >> k) & 1ull) {
-                    const uint32_t f1 = sort3(a, b, k), f2 = sort3(a, c, k), f3 = sort3(b, c, k);
-                    const bool m1 = vbit(col_dense(2, f1)), m2 = vbit(col_dense(2, f2)), m3 = vbit(col_dense(2, f3));
-                    const bool odd = !(m1 ^ m2 ^ m3);
-                    const bool rep = !(m1 && f1 < sp_) && !(m2 && f2 < sp_) && !(m3 && f3 < sp_);
-                    if (odd && rep) {
-                        const float dd = fmaxf(tri_diam(a, b, c), fmaxf(fmaxf(s.D[a][k], s.D[b][k]), s.D[c][k]));
-                        const uint64_t key = make_key(dd, tet_with(a, b, c, k));
-                        best = key < best ? key : best;
-                    }
-                }
+                const uint64_t cand = uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]);
+                const int C3a = c3(a), C3b = c3(b), C2a = c2(a), C2b = c2(b), C2c = c2(c);
+                const int ds = C3a + C2b + c;
+                const float dabc = __uint_as_float(uni(__float_as_uint(tri_diam(a, b, c))));
+                const bool on = (cand >> k) & 1ull;
+                const bool ga = k > a, gb = k > b, gc = k > c;
+                // dense indices of the facets {a,b,k}, {a,c,k}, {b,c,k} (colex == index order)
+                const int t11 = pin(c3k + C2a + b), t12 = pin(C3a + c2k + b), t13 = pin(C3a + C2b + k);
+                const int t21 = pin(c3k + C2a + c), t22 = pin(C3a + c2k + c), t23 = pin(C3a + C2c + k);
+                const int t31 = pin(c3k + C2b + c), t32 = pin(C3b + c2k + c), t33 = pin(C3b + C2c + k);
+                const int d1 = ga ? t11 : (gb ? t12 : t13);
+                const int d2 = ga ? t21 : (gc ? t22 : t23);
+                const int d3 = gb ? t31 : (gc ? t32 : t33);
+                const bool m1 = vbit(on ? d1 : 0), m2 = vbit(on ? d2 : 0), m3 = vbit(on ? d3 : 0);
+                const bool odd = !(m1 ^ m2 ^ m3);
+                const bool rep = !(m1 && d1 < ds) && !(m2 && d2 < ds) && !(m3 && d3 < ds);
+                const int ea = pin(ga ? c2k + a : C2a + k), eb = pin(gb ? c2k + b : C2b + k);
+                const int ec = pin(gc ? c2k + c : C2c + k);
+                const float dd = fmaxf(dabc, fmaxf(fmaxf(s.Dt[on ? ea : 0], s.Dt[on ? eb : 0]), s.Dt[on ? ec : 0]));
+                const uint32_t pabc = pack3(a, b, c);
+                const uint32_t p1 = pin(((uint32_t)k << 24) | pabc), p2 = pin(pack4(a, k, b, c));
+                const uint32_t p3 = pin(pack4(a, b, k, c)), p4 = pin((pabc << 8) | (uint32_t)k);
+                const uint32_t pk = ga ? p1 : (gb ? p2 : (gc ? p3 : p4));
+                const uint64_t key = make_key(dd, pk);
+                best = (on && odd && rep && key < best) ? key : best;
             }
         }
         return wave_min_u64(best);
@@ -354,26 +416,27 @@ struct Complex {
     __device__ bool v_toggle(int dim, uint32_t x, int& v) {
         const int lane = lane_id();
         const int idx = col_dense(dim, x);
-        if (vbit(idx)) {
+        if (uni(vbit(idx))) {
             int pos = -1;
+            v = (int)uni((uint32_t)v);
             for (int base = 0; base < v && pos < 0; base += kWave) {
                 const uint64_t bal = ballot(base + lane < v && s.vcur[base + lane] == x);
                 if (bal) pos = base + __ffsll((unsigned long long)bal) - 1;
             }
-            const uint32_t last = s.vcur[v - 1];
+            const uint32_t last = uni(s.vcur[v - 1]);
             lds_sync();
             if (lane == 0) {
                 s.vcur[pos] = last;
                 atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
             }
-            --v;
+            v = (int)uni((uint32_t)(v - 1));
         } else {
             if (v >= kVCap) return false;
             if (lane == 0) {
                 s.vcur[v] = x;
                 atomicOr(&s.vbits[idx >> 5], 1u << (idx & 31));
             }
-            ++v;
+            v = (int)uni((uint32_t)(v + 1));
         }
         lds_sync();
         return true;
@@ -384,49 +447,43 @@ struct Complex {
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
         if (nna > kNACap) { err |= kErrNA; return; }
-        // ---- sort by column key DESCENDING (rank sort; keys staged in LDS when they fit) ----
+        // ---- sort by column key DESCENDING (rank sort). Sorted (key, pivot) records go to LDS
+        // when they fit (they are read back one per column, in order), else to scratch.
+        const bool in_lds = nna <= kNALds;
+        uint64_t* sk = in_lds ? s.u.na.key : sp<uint64_t>(ScratchLayout::sna_key);
+        uint64_t* st = in_lds ? s.u.na.tau : sp<uint64_t>(ScratchLayout::sna_tau);
         {
-            uint64_t* keys = s.u.sort_keys;
             const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
             const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
-            uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
-            uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
-            const bool in_lds = nna <= kVStoreLds / 2;
-            if (in_lds) {
-                for (int i = lane; i < nna; i += kWave) keys[i] = gk[i];
-                lds_sync();
-            }
             for (int i = lane; i < nna; i += kWave) {
-                const uint64_t v = in_lds ? keys[i] : gk[i];
+                const uint64_t v = gk[i];
                 int rank = 0;
-                if (in_lds) {
-                    for (int u = 0; u < nna; ++u) rank += keys[u] > v;
-                } else {
-                    for (int u = 0; u < nna; ++u) rank += gk[u] > v;
-                }
+                for (int u = 0; u < nna; ++u) rank += gk[u] > v;
                 sk[rank] = v;
                 st[rank] = gt[i];
             }
             __syncthreads();
         }
-        const uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
-        const uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
+        DGN_SUB(16);
         uint32_t* gvmeta = sp<uint32_t>(ScratchLayout::vmeta);
         uint64_t* gpiv = sp<uint64_t>(ScratchLayout::piv);
         uint32_t* gvstore = sp<uint32_t>(ScratchLayout::vstore);
         int npiv = 0, vused = 0;
-        uint64_t nk = nna > 0 ? sk[0] : 0, nt = nna > 0 ? st[0] : 0;
+        uint64_t nk = nna > 0 ? uni64(sk[0]) : 0, nt = nna > 0 ? uni64(st[0]) : 0;
         for (int ci = 0; ci < nna; ++ci) {
             const uint64_t colkey = nk;
             uint64_t tau = nt;
             if (ci + 1 < nna) {  // prefetch the next column's record
-                nk = sk[ci + 1];
-                nt = st[ci + 1];
+                nk = uni64(sk[ci + 1]);
+                nt = uni64(st[ci + 1]);
             }
             const uint32_t cp = key_packed(colkey);
             const float birth = key_diam(colkey);
+            DGN_SUB(17);
             int owner = find_pivot(npiv, tau);
+            DGN_SUB(18);
             uint32_t app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+            DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
             if (owner >= 0 || app != kNone) {
                 v_toggle(dim, cp, v);
@@ -439,23 +496,27 @@ struct Complex {
                         if (!(column_key(dim, app) > colkey)) { err |= kErrOrder; return; }
                         ok = v_toggle(dim, app, v);
                     } else {
-                        const uint32_t m = owner < kPivLds ? s.vmeta[owner] : gvmeta[owner];
+                        const uint32_t m = uni(owner < kPivLds ? s.vmeta[owner] : gvmeta[owner]);
                         if (m & kLazyBit) {
                             ok = v_toggle(dim, m & ~kLazyBit, v);
                         } else {
-                            const int off = (int)(m >> 9), len = (int)(m & 511);
+                            const int off = (int)uni(m >> 9), len = (int)uni(m & 511);
                             for (int t = 0; t < len && ok; ++t) {
-                                const uint32_t x = off + t < kVStoreLds ? s.u.vstore[off + t] : gvstore[off + t];
+                                const uint32_t x = uni(off + t < kVStoreLds ? s.vstore[off + t] : gvstore[off + t]);
                                 ok = v_toggle(dim, x, v);
                             }
                         }
                     }
                     if (!ok) { err |= kErrWorkCol; return; }
                     ++n_adds;
+                    DGN_SUB(20);
                     tau = v > 0 ? pivot_of_V(dim, v) : kInf;
+                    DGN_SUB(21);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
                     owner = find_pivot(npiv, tau);
+                    DGN_SUB(18);
                     app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+                    DGN_SUB(19);
                     if (owner < 0 && app == kNone) break;  // tau is this column's pivot
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
@@ -491,13 +552,13 @@ struct Complex {
                 if (vused + v > kVStoreCap || v > 511) { err |= kErrR; return; }
                 for (int t = lane; t < v; t += kWave) {
                     const uint32_t x = s.vcur[t];
-                    if (vused + t < kVStoreLds) s.u.vstore[vused + t] = x;
+                    if (vused + t < kVStoreLds) s.vstore[vused + t] = x;
                     else gvstore[vused + t] = x;
                     const int idx = col_dense(dim, x);
                     atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
                 }
                 meta = ((uint32_t)vused << 9) | (uint32_t)v;
-                vused += v;
+                vused = (int)uni((uint32_t)(vused + v));
             }
             if (lane == 0) {
                 if (npiv < kPivLds) {
@@ -508,8 +569,9 @@ struct Complex {
                     gvmeta[npiv] = meta;
                 }
             }
-            ++npiv;
+            npiv = (int)uni((uint32_t)(npiv + 1));
             lds_sync();
+            DGN_SUB(22);
         }
     }
 };
@@ -528,11 +590,11 @@ struct Complex {
 #endif
 
 template <int NP>
-__global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
+__global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
     __shared__ int64_t chunk_s;
 #ifdef DGN_PHASE_TIMING
-    uint64_t ph[16] = {0};
+    uint64_t ph[24] = {0};
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();
@@ -579,6 +641,10 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 continue;
             }
             Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0, 0, 0};
+#ifdef DGN_PHASE_TIMING
+            cx.ph = ph;
+            cx.tprev = &t_prev;
+#endif
             DGN_PHASE(7);
             // ---- load the local cloud (betti_features.cpp:67-73) ----
             if (lane < n && bl.clouds) {
@@ -608,15 +674,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 // given f32 lower triangle (ripser_wrapper.cpp:20-24 packing)
                 const float* L = bl.lower + (int64_t)gi * ((int64_t)bl.cloud_stride * (bl.cloud_stride - 1) / 2);
                 const int tot = n * (n - 1) / 2;
-                for (int t = lane; t < tot; t += kWave) {
-                    int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
-                    while (i * (i - 1) / 2 > t) --i;
-                    while ((i + 1) * i / 2 <= t) ++i;
-                    const int j = t - i * (i - 1) / 2;
-                    s.D[i][j] = L[t];
-                    s.D[j][i] = L[t];
-                }
-                if (lane < n) s.D[lane][lane] = 0.0f;
+                for (int t = lane; t < tot; t += kWave) s.Dt[t] = L[t];  // same packing
             } else {
                 typedef double double4_t __attribute__((ext_vector_type(4)));
                 const int T = (n + 15) / 16;
@@ -636,12 +694,10 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int row = 16 * I + (lane >> 4) + 4 * r;
-                            if (row < n && col < n) {
+                            if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
                                 const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
                                 const double d2 = (s.u.cloud.sq[row] + s.u.cloud.sq[col]) - 2.0 * dot;
-                                const float d = row == col ? 0.0f : (float)sqrt(fmax(d2, 0.0));
-                                s.D[row][col] = d;
-                                s.D[col][row] = d;
+                                s.Dt[c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
                             }
                         }
                     }
@@ -654,7 +710,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                 uint64_t m = 0;
                 if (lane < n) {
                     for (int w2 = 0; w2 < n; ++w2)
-                        if (w2 != lane && s.D[lane][w2] <= cx.thr) m |= 1ull << w2;
+                        if (w2 != lane && cx.dist(lane, w2) <= cx.thr) m |= 1ull << w2;
                 }
                 s.adj[lane] = lane < n ? m : 0ull;
                 s.tree[lane] = 0ull;
@@ -727,6 +783,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
             DGN_PHASE(1);
             uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
             uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
+            uint32_t* mincof = cx.template sp<uint32_t>(ScratchLayout::mincof);
                     // ---- dim 1: one lane per column (non-tree edge) ----
             if (dim_max >= 1) {
                 int nna = 0;
@@ -737,8 +794,9 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                     uint64_t colkey = 0, best = kInf;
                     if (e < n_edges) {
                         const int i = s.edges[e] >> 8, j = s.edges[e] & 255;
+                        uint32_t mc = kNone;
                         if (!((s.tree[i] >> j) & 1ull)) {
-                            birth = s.D[i][j];
+                            birth = cx.dlow(i, j);
                             colkey = make_key(birth, pack2(i, j));
                             const uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
@@ -753,8 +811,10 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                                 } else {
                                     na_col = true;
                                 }
+                                mc = key_packed(best);
                             }
                         }
+                        mincof[edge_dense(i, j)] = mc;
                     }
                     cx.append_pairs(1, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
@@ -810,6 +870,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                         const int a = ea, b = eb;
                         const int c = __ffsll((unsigned long long)tmask) - 1;
                         tmask &= tmask - 1;
+                        uint32_t mc = kNone;
                         if (!cx.is_cleared(a, b, c)) {
                             birth = cx.tri_diam(a, b, c);
                             colkey = make_key(birth, pack3(a, b, c));
@@ -821,8 +882,10 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
                                 apparent = cx.max_facet(2, best, col_unused) == pack3(a, b, c);
                                 na_col = !apparent;
+                                mc = key_packed(best);
                             }
                         }
+                        mincof[tri_dense(a, b, c)] = mc;
                     }
                     cx.append_pairs(2, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
@@ -928,7 +991,7 @@ __global__ __launch_bounds__(kWave) void betti_kernel(BettiLaunch bl) {
     }
 #ifdef DGN_PHASE_TIMING
     if (lane == 0 && bl.phase_cycles)
-        for (int k = 0; k < 16; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
+        for (int k = 0; k < 24; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
 #endif
 }
 

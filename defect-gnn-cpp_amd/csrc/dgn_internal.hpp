@@ -66,7 +66,7 @@ struct BettiLaunch {
     // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
     float* pairs_out;
     int32_t pair_cap;
-    unsigned long long* phase_cycles;  // [16] diagnostics build only (DGN_PHASE_TIMING)
+    unsigned long long* phase_cycles;  // [24] diagnostics build only (DGN_PHASE_TIMING)
 };
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();

@@ -24,15 +24,17 @@ ctx.host_betti(batch, rc)  # warm-up
 t0 = time.perf_counter()
 f, c = ctx.host_betti(batch, rc)
 dt = time.perf_counter() - t0
-ph = (C.c_ulonglong * 16)()
+ph = (C.c_ulonglong * 24)()
 dgn.lib().dgn_diag_phase_cycles(ctx.h, ph)
 ph = list(ph)
 names = ["load+gram", "adj+prim+edges", "dim1 apparent", "dim1 serial", "dim2 apparent", "dim2 serial",
          "stats+write", "dequeue/gap"]
-tot = sum(ph[:8])
+sub = ["serial:sort", "serial:col-start", "serial:find_pivot", "serial:apparent_owner", "serial:toggles", "serial:pivot_of_V", "serial:finalize"]
+tot = sum(ph[:8]) + sum(ph[16:23])
 out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round(dt, 4),
        "cycles_per_complex": round(tot / A), "phase_cycles_per_complex": {n: round(ph[i] / A) for i, n in enumerate(names)},
        "phase_share": {n: round(ph[i] / tot, 4) for i, n in enumerate(names)},
        "na1_per_complex": ph[8] / A, "na2_per_complex": ph[9] / A, "adds1": ph[10] / A, "adds2": ph[11] / A,
-       "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13]}
+       "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13],
+       "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
 print(json.dumps(out, indent=1))
