@@ -9,7 +9,27 @@ LIB      := $(PKG)/lib/libdgn.so
 
 KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/dgn_api.o
 
-all: $(LIB) oracle
+all: $(LIB) facade oracle
+
+# C++ facade mirroring the reference include/graph + include/topology API over the C ABI
+FDIR     := $(PKG)/cpp
+FBUILD   := $(PKG)/build/facade
+FACADE   := $(PKG)/lib/libdgn_facade.so
+FBIN     := $(PKG)/bin
+CXX      ?= g++
+FFLAGS   := -O2 -std=c++17 -fPIC -Wall -Wextra -Iinclude -I$(FDIR)/include
+FSRCS    := $(wildcard $(FDIR)/src/*.cpp)
+FOBJS    := $(patsubst $(FDIR)/src/%.cpp,$(FBUILD)/%.o,$(FSRCS))
+FHDRS    := $(shell find $(FDIR)/include -name '*.hpp') include/dgn.h
+facade: $(FACADE) $(FBIN)/preprocess_betti $(FBIN)/facade_check
+$(FBUILD)/%.o: $(FDIR)/src/%.cpp $(FHDRS)
+	@mkdir -p $(FBUILD)
+	$(CXX) $(FFLAGS) -c $< -o $@
+$(FACADE): $(FOBJS) $(LIB)
+	$(CXX) -shared -o $@ $(FOBJS) -L$(PKG)/lib -ldgn -Wl,-rpath,'$$ORIGIN'
+$(FBIN)/%: $(FDIR)/tools/%.cpp $(FACADE) $(FHDRS)
+	@mkdir -p $(FBIN)
+	$(CXX) $(FFLAGS) -o $@ $< -L$(PKG)/lib -ldgn_facade -ldgn -Wl,-rpath,'$$ORIGIN/../lib'
 
 $(BUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(BUILD)
@@ -41,7 +61,7 @@ $(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/dgn_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(DBUILD) $(DIAG)
+	rm -rf $(BUILD) $(LIB) $(DBUILD) $(DIAG) $(FACADE) $(FBIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean diag
+.PHONY: all oracle clean diag facade

@@ -180,7 +180,10 @@ RbfSpec make_rbf(const dgn_graph_params* p) {
 }
 
 // graph counting pass shared by the graph and Betti entry points
-int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, double eps, int64_t* num_edges) {
+// `betti` = the neighbour pass internal to dgn_*_betti (timed under its own names so the graph
+// kernels' roofline is never mixed with it)
+int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, double eps, int64_t* num_edges,
+                     bool betti = false) {
     const int64_t A = b->num_atoms, B = b->num_structures;
     const int64_t nblocks = graph_blocks(A);
     HIP_TRY(c, c->meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
@@ -190,17 +193,17 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(sc, 0, sizeof(Scalars), c->stream));
     {
-        TimedLaunch t(c, "prep_structures", (double)B * (72 + 16), 0);
+        TimedLaunch t(c, betti ? "betti_nl_prep" : "prep_structures", (double)B * (72 + 16), 0);
         HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, B, rc, c->meta.as<StructMeta>()));
     }
     GraphLaunch g{c->meta.as<StructMeta>(), b->atom_offset, b->positions, B, A, rc * rc, eps, kmax};
     {
-        TimedLaunch t(c, "graph_count", (double)A * (24 + 4), 0);
+        TimedLaunch t(c, betti ? "betti_nl_count" : "graph_count", (double)A * (24 + 4), 0);
         HIP_TRY(c, launch_graph_count(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
                                       &sc->max_candidates, &sc->sum_sq));
     }
     {
-        TimedLaunch t(c, "block_scan", (double)nblocks * 16, 0);
+        TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 16, 0);
         HIP_TRY(c, launch_block_scan(c->stream, c->block_sums.as<int64_t>(), nblocks, &sc->total));
     }
     HIP_TRY(c, hipMemcpyAsync(c->host_scalars, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
@@ -220,7 +223,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
 }
 
 int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int32_t* col, double* dist,
-                    double* disp, void* rbf, const RbfSpec& rs) {
+                    double* disp, void* rbf, const RbfSpec& rs, bool betti = false) {
     if (!c->have_count || c->cnt_pos != b->positions || c->cnt_atoms != b->num_atoms)
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
     const int cap = graph_emit_cap(c->cnt_max_candidates);
@@ -236,7 +239,7 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     const double bytes = A * 24 + (double)c->cnt_structs * 72 + 8 * (A + 1) + 4 * A + E * (4 + (dist ? 8 : 0)) +
                          (disp ? 24 * E : 0) + (rbf ? E * rs.nbins * rbf_bytes : 0);
     {
-        TimedLaunch t(c, "graph_emit", bytes, 0);
+        TimedLaunch t(c, betti ? "betti_nl_emit" : "graph_emit", bytes, 0);
         HIP_TRY(c, launch_graph_emit(c->stream, g, cap, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
                                      const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs, &sc->error_flag));
     }
@@ -262,7 +265,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     int max_points = cloud_stride;
     if (!given) {
         int64_t E = 0;
-        int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E);
+        int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E, true);
         if (st) return st;
         HIP_TRY(c, c->b_row_ptr.ensure(sizeof(int64_t) * (size_t)(A + 1)));
         HIP_TRY(c, c->b_col.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(E, 1)));
@@ -271,7 +274,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         RbfSpec none{};
         none.dtype = DGN_NONE;
         st = graph_emit_impl(c, b, c->b_row_ptr.as<int64_t>(), c->b_col.as<int32_t>(), c->b_dist.as<double>(),
-                             c->b_disp.as<double>(), nullptr, none);
+                             c->b_disp.as<double>(), nullptr, none, true);
         if (st) return st;
         max_points = (int)c->cnt_max_candidates + 1;
     }

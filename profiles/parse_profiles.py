@@ -1,0 +1,81 @@
+"""Fold one round's rocprofv3 output (profiles/collect.sh) into committed summaries:
+  profiles/<round>_kernel_stats.csv   rocprofv3 --stats table of the default bench
+  profiles/<round>_summary.json       per-kernel avg duration + PMC HBM bytes per graph-emit launch
+  profiles/traffic_latest.json        what bench.py reads for roofline.traffic
+HBM bytes per launch = 2 x FETCH_SIZE (gfx950 tallies 128-B read requests at 64 B,
+MI355X_MICROARCH.md "HBM") + WRITE_SIZE (exact for wide streaming stores); FETCH/WRITE_SIZE are in KB.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def find(d, pattern):
+    hits = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    return hits[-1] if hits else None
+
+
+def pmc_per_launch(path, kernel_substr, counter):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--dir", required=True)
+    a = ap.parse_args()
+    summary = {"round": a.round}
+    stats = find(os.path.join(a.dir, "trace"), "*kernel_stats.csv")
+    if stats:
+        shutil.copy(stats, os.path.join(HERE, f"{a.round}_kernel_stats.csv"))
+        with open(stats) as f:
+            summary["kernel_stats"] = {r["Name"]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                                                   "total_ns": float(r["TotalDurationNs"]),
+                                                   "percent": float(r["Percentage"])} for r in csv.DictReader(f)}
+    for name in ("trace_bench", "fetch_bench", "write_bench"):
+        p = os.path.join(a.dir, f"{name}.json")
+        if os.path.exists(p):
+            lines = [l for l in open(p) if l.startswith("{")]
+            if lines:
+                summary[name] = json.loads(lines[-1])
+    fetch = find(os.path.join(a.dir, "fetch"), "*counter_collection.csv")
+    write = find(os.path.join(a.dir, "write"), "*counter_collection.csv")
+    if fetch and write:
+        fv = pmc_per_launch(fetch, "graph_emit_kernel", "FETCH_SIZE")
+        wv = pmc_per_launch(write, "graph_emit_kernel", "WRITE_SIZE")
+        if fv and wv:
+            f_kb = sum(fv) / len(fv)
+            w_kb = sum(wv) / len(wv)
+            hbm = 2 * f_kb * 1024 + w_kb * 1024
+            gb = summary.get("fetch_bench", {})
+            cfg = gb.get("config", {})
+            emit = summary.get("trace_bench", {}).get("roofline") or {}
+            key = None
+            if cfg:
+                # must match bench.py's workload_key for the default run
+                key = "fcc4x%d_rc5.0_k20_nb50" % cfg.get("structures_per_gpu", 0)
+            summary["graph_emit_pmc"] = {"launches": len(fv), "fetch_kb": f_kb, "write_kb": w_kb,
+                                         "hbm_bytes_per_launch": hbm,
+                                         "algorithmic_bytes_per_launch": emit.get("algorithmic_bytes_per_launch"),
+                                         "workload_key": key}
+            with open(os.path.join(HERE, "traffic_latest.json"), "w") as f:
+                json.dump({"round": a.round, "workload_key": key, "hbm_bytes_per_launch": hbm,
+                           "fetch_kb_x2": 2 * f_kb, "write_kb": w_kb,
+                           "source": f"profiles/{a.round}_summary.json"}, f, indent=1)
+    with open(os.path.join(HERE, f"{a.round}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    print(json.dumps({k: v for k, v in summary.items() if k != "kernel_stats"}, indent=1)[:4000])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+"""C++ facade (defect-gnn-cpp_amd/cpp, libdgn_facade.so) — the reference's include/graph and
+include/topology API (same names, defaults, column-major shapes) over the C ABI.
+
+CPU tests: POSCAR parsing + Structure (vasp_parser.cpp:13-78, structure.cpp:7-66), the Betti .bin
+format (betti_features.cpp:121-153), PCA fit/transform/save/load (pca.cpp:15-121) against numpy.
+GPU tests: tools/facade_check drives NeighborList, CrystalGraph, gaussian_rbf,
+compute_persistence_from_distances, compute_atom_betti_features and
+compute_structure_betti_features on the reference's POSCARs and compares with the golden
+fixtures / the oracle; tools/preprocess_betti is run end to end.
+"""
+import glob
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+
+BIN = os.path.join(ROOT, "defect-gnn-cpp_amd", "bin")
+POSCARS = os.path.join(GOLDEN, "poscar")
+
+
+def _run(args, timeout=300):
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    return r.returncode, r.stdout, r.stderr
+
+
+def _read(path):
+    out = {}
+    for line in open(path):
+        parts = line.split()
+        key, n = parts[0], int(parts[1])
+        out[key] = np.array([float(x) for x in parts[2:2 + n]])
+    return out
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(os.path.join(GOLDEN, "poscar_rc5.npz"))
+
+
+@pytest.mark.parametrize("name", ["1", "741", "1046_1", "741_2"])
+def test_parse_poscar_matches_fixture(tmp_path, golden, name):
+    out = tmp_path / "p.txt"
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), "parse", os.path.join(POSCARS, f"{name}.vasp"), str(out)])
+    assert rc == 0, err
+    d = _read(out)
+    lat = golden[f"{name}/lattice"]
+    pos = golden[f"{name}/positions"]
+    assert np.array_equal(d["lattice"].reshape(3, 3), lat)
+    assert np.array_equal(d["positions"].reshape(-1, 3), pos)
+    assert np.array_equal(d["species"].astype(np.int32), golden[f"{name}/species"])
+    assert d["counts"].sum() == pos.shape[0]
+    # compute_distance_matrix: minimum-image distances, symmetric, zero diagonal
+    n = pos.shape[0]
+    dm = d["distance_matrix"].reshape(n, n, order="F")
+    assert np.array_equal(dm, dm.T) and not np.any(np.diag(dm))
+    frac = d["frac"].reshape(-1, 3)
+    df = frac[None, :, :] - frac[:, None, :]
+    a = np.abs(df)  # std::round: halves away from zero (floor(x + 0.5) misrounds 0.49999999999999994)
+    r = np.floor(a)
+    df -= np.sign(df) * (r + (a - r >= 0.5))
+    ref = np.sqrt(((df @ lat) ** 2).sum(-1))
+    np.testing.assert_allclose(dm, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_parse_missing_file_raises(tmp_path):
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), "parse", str(tmp_path / "nope.vasp"), str(tmp_path / "o")])
+    assert rc == 1 and "Could not open file" in err
+
+
+def _write_bin(path, m):
+    """save_betti_features layout: int32 rows, int32 cols, f64 column-major."""
+    with open(path, "wb") as f:
+        f.write(np.array(m.shape, np.int32).tobytes())
+        f.write(np.asfortranarray(m).tobytes(order="F"))
+
+
+def test_pca_matches_numpy(tmp_path):
+    rng = np.random.default_rng(7)
+    x = rng.normal(size=(400, 35)) @ rng.normal(size=(35, 35)) + rng.normal(size=35)
+    _write_bin(tmp_path / "x.bin", x)
+    out = tmp_path / "pca.txt"
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), "pca", str(tmp_path / "x.bin"), "6", str(out)])
+    assert rc == 0, err
+    d = _read(out)
+    mean = x.mean(0)
+    np.testing.assert_allclose(d["mean"], mean, rtol=1e-12)
+    xc = x - mean
+    _, s, vt = np.linalg.svd(xc, full_matrices=False)
+    var = s ** 2 / (x.shape[0] - 1)
+    np.testing.assert_allclose(d["ratio"], var[:6] / var.sum(), rtol=1e-9)
+    comp = d["components"].reshape(35, 6, order="F")
+    for c in range(6):  # unique up to sign; the build makes the largest |coefficient| positive
+        v = vt[c] * np.sign(vt[c][np.argmax(np.abs(vt[c]))])
+        np.testing.assert_allclose(comp[:, c], v, atol=1e-9)
+    np.testing.assert_allclose(d["transform"].reshape(-1, 6, order="F"), xc @ comp, atol=1e-9)
+
+
+def test_pca_rejects_wrong_width(tmp_path):
+    _write_bin(tmp_path / "x.bin", np.ones((5, 7)))
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), "pca", str(tmp_path / "x.bin"), "2", str(tmp_path / "o")])
+    assert rc == 1 and "correct number of columns" in err
+
+
+def test_gpu_entry_fails_loudly_without_device(tmp_path):
+    """No GPU here: the facade must raise (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), os.path.join(POSCARS, "741.vasp"), "5", "20",
+                       str(tmp_path / "o.txt")])
+    assert rc == 1 and "device" in err.lower(), err
+
+
+# ------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["1", "741"])
+def test_facade_graph_and_betti(tmp_path, golden, name):
+    import oracle_py as O
+    out = tmp_path / "f.txt"
+    rc, _, err = _run([os.path.join(BIN, "facade_check"), os.path.join(POSCARS, f"{name}.vasp"), "5", "20", str(out)])
+    assert rc == 0, err
+    d = _read(out)
+    n = golden[f"{name}/positions"].shape[0]
+    # NeighborList(rc=5, K=20): bit-exact CSR (tie-free POSCARs)
+    assert np.array_equal(d["row_ptr"].astype(np.int64), golden[f"{name}/k20/row_ptr"])
+    assert np.array_equal(d["col"].astype(np.int32), golden[f"{name}/k20/col"])
+    assert np.array_equal(d["dist"], golden[f"{name}/k20/dist"])
+    E = d["col"].size
+    # CrystalGraph: node features by species, edge_index 2 x E, edge_attr E x 50 column-major f64
+    sp = golden[f"{name}/species"]
+    nf = d["node_features"].reshape(n, 4, order="F")
+    assert np.array_equal(nf[:, 0], 10.0 * sp) and np.array_equal(nf[:, 3], 10.0 * sp + 3)
+    ei = d["edge_index"].reshape(2, E, order="F")
+    rows = np.repeat(np.arange(n), np.diff(golden[f"{name}/k20/row_ptr"]))
+    assert np.array_equal(ei[0], rows) and np.array_equal(ei[1], golden[f"{name}/k20/col"])
+    ea = d["edge_attr"].reshape(E, 50, order="F")
+    ref = np.stack([O.gaussian_rbf(x, 5.0, 0.1) for x in d["dist"]])
+    np.testing.assert_allclose(ea, ref, rtol=1e-12)  # f64 path: 1e-6 is the contract
+    np.testing.assert_allclose(d["rbf_one"], O.gaussian_rbf(1.2345, 5.0, 0.1), rtol=1e-12)
+    # compute_structure_betti_features: N x 35 column-major vs verbatim-Ripser fixtures
+    feat = d["betti"].reshape(n, 35, order="F")
+    np.testing.assert_allclose(feat, golden[f"{name}/betti5/features"], rtol=1e-6, atol=1e-12)
+    # single-atom path equals row 0 of the batched path
+    np.testing.assert_allclose(d["atom0"], feat[0], rtol=1e-6, atol=1e-12)
+    # compute_persistence_from_distances on atom 0's cloud vs the oracle on the same f32 matrix
+    m = d["cloud0"].size // 3
+    cloud = d["cloud0"].reshape(m, 3, order="F")
+    dm = np.sqrt(((cloud[:, None, :] - cloud[None, :, :]) ** 2).sum(-1))
+    lower = np.concatenate([dm[i, :i] for i in range(1, m)]).astype(np.float32)
+    po = O.persistence(lower, m, np.float32(5.0))
+    pd0 = d["pd0"].reshape(-1, 2)
+    fin = pd0[np.isfinite(pd0[:, 1])]
+    assert len(pd0) - len(fin) == po["n_inf0"]
+    for got, exp in ((fin, po["dim0"]), (d["pd1"].reshape(-1, 2), po["dim1"]), (d["pd2"].reshape(-1, 2), po["dim2"])):
+        key = lambda a: a[np.lexsort((a[:, 1], a[:, 0]))]
+        assert np.array_equal(key(got.astype(np.float32)), key(np.asarray(exp, np.float32)))
+    assert d["bin_roundtrip"][0] == 1.0
+
+
+@pytest.mark.gpu
+def test_preprocess_driver(tmp_path, golden):
+    """preprocess_betti over the POSCAR fixtures at rc=5: one betti/<id>.bin per structure,
+    identical (<=1e-6) to the verbatim-Ripser fixtures, plus a loadable pca_model.bin."""
+    outdir = tmp_path / "processed"
+    rc, _, err = _run([os.path.join(BIN, "preprocess_betti"), POSCARS, str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    for path in sorted(glob.glob(os.path.join(POSCARS, "*.vasp"))):
+        sid = os.path.splitext(os.path.basename(path))[0]
+        raw = open(outdir / "betti" / f"{sid}.bin", "rb").read()
+        r, c = np.frombuffer(raw[:8], np.int32)
+        feat = np.frombuffer(raw[8:], np.float64).reshape(r, c, order="F")
+        assert c == 35 and r == golden[f"{sid}/positions"].shape[0]
+        if f"{sid}/betti5/features" in golden:
+            np.testing.assert_allclose(feat, golden[f"{sid}/betti5/features"], rtol=1e-6, atol=1e-12)
+    raw = open(outdir / "pca_model.bin", "rb").read()
+    assert np.frombuffer(raw[:4], np.int32)[0] == 6
