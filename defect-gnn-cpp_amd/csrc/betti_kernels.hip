@@ -601,13 +601,16 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;
 
+    // complexes of this launch: all of them, or the overflow list written by the bucket pass
+    const int64_t total = bl.work_list ? (int64_t)*bl.overflow_len : A;
     for (;;) {
-        if (lane == 0) chunk_s = (int64_t)atomicAdd((unsigned int*)bl.work_counter, 1u) * kChunk;
+        if (lane == 0) chunk_s = (int64_t)atomicAdd((unsigned int*)bl.queue, 1u) * kChunk;
         __syncthreads();
         const int64_t chunk0 = chunk_s;
         __syncthreads();
-        if (chunk0 >= A) break;
-        for (int64_t gi = chunk0; gi < chunk0 + kChunk && gi < A; ++gi) {
+        if (chunk0 >= total) break;
+        for (int64_t wi = chunk0; wi < chunk0 + kChunk && wi < total; ++wi) {
+            const int64_t gi = bl.work_list ? (int64_t)bl.work_list[wi] : wi;
             int64_t r0 = 0;
             int n;
             if (bl.clouds || bl.lower) {
@@ -617,6 +620,13 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 n = (int)(bl.row_ptr[gi + 1] - r0) + 1;
             }
             double* feat = bl.features ? bl.features + 35 * gi : nullptr;
+            if (n > NP) {
+                if (bl.skip_above) continue;  // reduced by the overflow launch
+                if (lane == 0) atomicOr(bl.error_flag, kErrTooManyPoints);
+                if (feat && lane < 35) feat[lane] = __builtin_nan("");
+                if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
+                continue;
+            }
             // structure of gi and the 1/count weight (betti_features.cpp:62-63, 77)
             double weight = 1.0;
             if (bl.species) {
@@ -634,12 +644,6 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 weight = 1.0 / (double)cnt;
             }
 
-            if (n > NP) {
-                if (lane == 0) atomicOr(bl.error_flag, kErrTooManyPoints);
-                if (feat && lane < 35) feat[lane] = __builtin_nan("");
-                if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
-                continue;
-            }
             Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0, 0, 0};
 #ifdef DGN_PHASE_TIMING
             cx.ph = ph;
@@ -1011,26 +1015,69 @@ int betti_grid_waves(int device) {
     return prop.multiProcessorCount * per_cu;
 }
 
-hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves) {
-    const int np = np_for(max_points);
-    int per_cu = 0;
-    hipError_t e = hipSuccess;
-    int dev = 0;
+// route complexes with more than np_small points to the overflow list (wave-aggregated append)
+__global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small) {
+    const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int n = 0;
+    if (gi < bl.num_atoms)
+        n = (bl.clouds || bl.lower) ? bl.npoints[gi] : (int)(bl.row_ptr[gi + 1] - bl.row_ptr[gi]) + 1;
+    const bool big = gi < bl.num_atoms && n > np_small;
+    const uint64_t bal = ballot(big);
+    if (!bal) return;
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(bl.overflow_len, (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl((int)base, leader, kWave);
+    if (big) bl.overflow_list[base + mask_prefix(bal)] = (int32_t)gi;
+}
+
+template <int NP>
+static hipError_t launch_np(hipStream_t st, const BettiLaunch& b, int grid_waves, int64_t max_items) {
+    int dev = 0, per_cu = 0;
+    hipError_t e;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return e;
-    if (np == 32) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<32>, kWave, 0);
-    else if (np == 48) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<48>, kWave, 0);
-    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<64>, kWave, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, 0);
     if (e != hipSuccess || per_cu <= 0) per_cu = 4;
     int grid = prop.multiProcessorCount * per_cu;
     if (grid > grid_waves) grid = grid_waves;
-    const int64_t chunks = (b.num_atoms + kChunk - 1) / kChunk;
+    const int64_t chunks = (max_items + kChunk - 1) / kChunk;
     if (grid > chunks) grid = (int)(chunks > 0 ? chunks : 1);
-    if (np == 32) hipLaunchKernelGGL(betti_kernel<32>, dim3(grid), dim3(kWave), 0, st, b);
-    else if (np == 48) hipLaunchKernelGGL(betti_kernel<48>, dim3(grid), dim3(kWave), 0, st, b);
-    else hipLaunchKernelGGL(betti_kernel<64>, dim3(grid), dim3(kWave), 0, st, b);
+    hipLaunchKernelGGL(betti_kernel<NP>, dim3(grid), dim3(kWave), 0, st, b);
     return hipGetLastError();
+}
+
+static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int grid_waves, int64_t max_items) {
+    if (np == 32) return launch_np<32>(st, b, grid_waves, max_items);
+    if (np == 48) return launch_np<48>(st, b, grid_waves, max_items);
+    return launch_np<64>(st, b, grid_waves, max_items);
+}
+
+// Two-level dispatch: the main launch uses the instantiation sized for typical complexes
+// (NP <= 48: about half the LDS of NP = 64, so twice the resident waves); complexes above it
+// are listed by betti_bucket_kernel and reduced by an NP = 64 launch. Counters and the list
+// length live on the device, so nothing synchronizes with the host in between.
+hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves) {
+    const int np_big = np_for(max_points);
+    const int np_main = np_big > 48 ? 48 : np_big;
+    BettiLaunch m = b;
+    m.work_list = nullptr;
+    m.queue = b.work_counter;
+    m.skip_above = np_big > np_main ? 1 : 0;
+    if (m.skip_above) {
+        const int64_t blocks = (b.num_atoms + 255) / 256;
+        hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = launch_for(np_main, st, m, grid_waves, b.num_atoms);
+    if (e != hipSuccess || !m.skip_above) return e;
+    BettiLaunch o = b;
+    o.work_list = b.overflow_list;
+    o.queue = b.work_counter2;
+    o.skip_above = 0;
+    return launch_for(np_big, st, o, grid_waves, b.num_atoms);
 }
 
 }  // namespace dgn

@@ -60,8 +60,10 @@ struct Scalars {  // device-side scalars, one allocation
     unsigned long long sum_sq;  // sum over atoms of (candidates + 1)^2
     uint32_t max_candidates;
     uint32_t error_flag;
-    uint32_t work_counter;
-    uint32_t pad;
+    uint32_t work_counter;   // betti main launch queue
+    uint32_t work_counter2;  // betti overflow launch queue
+    uint32_t overflow_len;   // complexes routed to the overflow launch
+    uint32_t pad[3];
 };
 
 }  // namespace
@@ -84,7 +86,7 @@ struct dgn_ctx {
     int64_t cnt_edges = 0;
     double cnt_sum_sq = 0;
     // betti workspace
-    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch;
+    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list;
     int betti_slots = 0;
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
@@ -288,7 +290,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
     sc = c->scalars.as<Scalars>();
-    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 2 * sizeof(uint32_t), c->stream));
+    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 4 * sizeof(uint32_t), c->stream));
+    HIP_TRY(c, c->b_list.ensure(sizeof(int32_t) * (size_t)A));
     BettiLaunch bl{};
     bl.row_ptr = given ? nullptr : c->b_row_ptr.as<int64_t>();
     bl.disp = given ? nullptr : c->b_disp.as<double>();
@@ -302,6 +305,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.counts = counts;
     bl.error_flag = &sc->error_flag;
     bl.work_counter = &sc->work_counter;
+    bl.work_counter2 = &sc->work_counter2;
+    bl.overflow_list = c->b_list.as<int32_t>();
+    bl.overflow_len = &sc->overflow_len;
     bl.scratch = c->b_scratch.as<uint8_t>();
     bl.scratch_per_wave = spw;
     bl.clouds = clouds;
@@ -412,7 +418,7 @@ void dgn_ctx_destroy(dgn_ctx* c) {
     fold_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
     for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
-                      &c->b_disp, &c->b_scratch, &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
+                      &c->b_disp, &c->b_scratch, &c->b_list, &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
         b->release();
     if (c->host_scalars) (void)hipHostFree(c->host_scalars);
     if (c->own) (void)hipStreamDestroy(c->own);

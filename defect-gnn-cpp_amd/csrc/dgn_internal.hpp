@@ -54,7 +54,13 @@ struct BettiLaunch {
     double* features;         // [A][35]
     int32_t* counts;          // [A][4] or null
     uint32_t* error_flag;
-    uint32_t* work_counter;   // persistent work queue
+    uint32_t* work_counter;   // persistent work queue (main launch)
+    uint32_t* work_counter2;  // persistent work queue (overflow launch)
+    // complexes larger than the main instantiation's NP are listed here by a bucket pass and
+    // reduced by a second, wider launch (so one rare large complex does not put the whole batch
+    // on the low-occupancy instantiation)
+    int32_t* overflow_list;   // [num_atoms]
+    uint32_t* overflow_len;
     uint8_t* scratch;         // per-wave global scratch
     int64_t scratch_per_wave;
     // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
@@ -67,6 +73,10 @@ struct BettiLaunch {
     float* pairs_out;
     int32_t pair_cap;
     unsigned long long* phase_cycles;  // [24] diagnostics build only (DGN_PHASE_TIMING)
+    // set by launch_betti per launch
+    const int32_t* work_list; // null = all complexes 0..num_atoms-1
+    uint32_t* queue;          // work counter of this launch
+    int32_t skip_above;       // 1 = complexes above NP are left to the overflow launch
 };
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();

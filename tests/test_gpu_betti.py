@@ -111,3 +111,41 @@ def test_persistence_from_distance_matrix(ctx):
         r = refs[c]
         assert np.array_equal(pairs[c, 1, :counts[c, 2]], r["dim1"]) and np.array_equal(pairs[c, 2, :counts[c, 3]], r["dim2"])
         assert np.array_equal(pairs[c, 0, :counts[c, 0]], r["dim0"])
+
+
+def test_mixed_sizes_two_level_dispatch(ctx):
+    """Complexes of 2..64 points in one batch: <= 48 go to the main launch, the rest through
+    the bucket pass to the NP = 64 overflow launch; every complex must match the oracle."""
+    rng = np.random.default_rng(11)
+    C, maxp = 160, 64
+    clouds = np.zeros((C, maxp, 3))
+    npts = rng.integers(2, maxp + 1, size=C).astype(np.int32)
+    npts[:8] = maxp  # guarantee overflow members
+    for c in range(C):
+        clouds[c, :npts[c]] = rng.uniform(0, 4.5, size=(npts[c], 3))
+    pairs, counts = ctx.host_persistence(clouds, npts, 2.5, cap=1024)
+    for c in range(C):
+        n = npts[c]
+        r = O.persistence(O.local_distances(clouds[c, :n]), n, np.float32(2.5))
+        assert counts[c, 1] == r["n_inf0"], c
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+
+
+def test_betti_batch_with_dense_outlier(ctx):
+    """A compressed FCC cell (about 50 neighbours within rc) inside a batch of ordinary ones:
+    its atoms take the overflow launch, the others the main launch."""
+    batch = dgn.synth_batch("fcc", 4, 3)
+    n = 256
+    batch["lattice"][1] *= 0.95
+    batch["positions"][n:2 * n] *= 0.95
+    f, c = ctx.host_betti(batch, 5.0)
+    sizes = []
+    for s in range(3):
+        sl = slice(s * n, (s + 1) * n)
+        nl = O.neighbor_list(batch["lattice"][s], batch["positions"][sl], 5.0, None)
+        sizes.append(int(np.diff(nl["row_ptr"]).max()) + 1)
+        fo, co = O.structure_betti(batch["lattice"][s], batch["positions"][sl], batch["species"][sl], 5.0)
+        assert np.array_equal(c[sl], co), s
+        np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
+    assert sizes[1] > 48 and max(sizes[0], sizes[2]) <= 48, sizes
