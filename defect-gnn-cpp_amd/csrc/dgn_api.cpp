@@ -74,7 +74,8 @@ struct dgn_ctx {
     hipStream_t stream = nullptr;
     std::string last_error;
     // graph workspace
-    DevBuf meta, counts, block_sums, scalars;
+    DevBuf meta, counts, block_sums, block_aux, atom_struct, rows_d, rows_j, scalars;
+    bool cnt_rows = false;  // the count pass stored ranked rows (streaming emit path)
     Scalars* host_scalars = nullptr;  // pinned
     // count->emit handshake
     bool have_count = false;
@@ -178,6 +179,8 @@ RbfSpec make_rbf(const dgn_graph_params* p) {
     const double sigma = p->rbf_cutoff / 3;
     r.inv_sigma2 = 1 / std::pow(sigma, 2);
     r.norm = 1 / (sigma * std::sqrt(2 * M_PI));
+    r.inv_nbins = r.nbins > 0 ? 1.0f / (float)r.nbins : 0.0f;
+    r.norm_f = (float)r.norm;
     return r;
 }
 
@@ -191,22 +194,34 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     HIP_TRY(c, c->meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
     HIP_TRY(c, c->counts.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
     HIP_TRY(c, c->block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, c->block_aux.ensure(2 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, c->atom_struct.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(sc, 0, sizeof(Scalars), c->stream));
     {
         TimedLaunch t(c, betti ? "betti_nl_prep" : "prep_structures", (double)B * (72 + 16), 0);
-        HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, B, rc, c->meta.as<StructMeta>()));
+        HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, B, rc, c->meta.as<StructMeta>(),
+                                          c->atom_struct.as<int32_t>()));
     }
-    GraphLaunch g{c->meta.as<StructMeta>(), b->atom_offset, b->positions, B, A, rc * rc, eps, kmax};
+    GraphLaunch g{c->meta.as<StructMeta>(), c->atom_struct.as<int32_t>(), b->atom_offset, b->positions, B, A,
+                  rc * rc, eps, kmax};
+    // stored-rows path: the count pass ranks and keeps each atom's rows, the emit pass streams
+    const bool rows = !betti && kmax > 0 && kmax <= (uint64_t)kRowsMaxK && A > 0;
+    if (rows) {
+        HIP_TRY(c, c->rows_d.ensure(sizeof(uint64_t) * (size_t)A * (size_t)kmax));
+        HIP_TRY(c, c->rows_j.ensure(sizeof(uint64_t) * (size_t)A * (size_t)kmax));
+    }
     {
         TimedLaunch t(c, betti ? "betti_nl_count" : "graph_count", (double)A * (24 + 4), 0);
         HIP_TRY(c, launch_graph_count(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
-                                      &sc->max_candidates, &sc->sum_sq));
+                                      c->block_aux.as<uint64_t>(), rows ? c->rows_d.as<uint64_t>() : nullptr,
+                                      rows ? c->rows_j.as<uint64_t>() : nullptr));
     }
     {
         TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 16, 0);
-        HIP_TRY(c, launch_block_scan(c->stream, c->block_sums.as<int64_t>(), nblocks, &sc->total));
+        HIP_TRY(c, launch_block_scan(c->stream, c->block_sums.as<int64_t>(), c->block_aux.as<uint64_t>(), nblocks,
+                                     &sc->total, &sc->max_candidates, &sc->sum_sq));
     }
     HIP_TRY(c, hipMemcpyAsync(c->host_scalars, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -220,6 +235,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     c->cnt_max_candidates = c->host_scalars->max_candidates;
     c->cnt_edges = c->host_scalars->total;
     c->cnt_sum_sq = (double)c->host_scalars->sum_sq;
+    c->cnt_rows = rows && c->cnt_max_candidates <= (uint32_t)kRowsCap;
     if (num_edges) *num_edges = c->cnt_edges;
     return DGN_OK;
 }
@@ -234,12 +250,25 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     if (b->num_atoms == 0) return DGN_OK;
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, sizeof(uint32_t), c->stream));
-    GraphLaunch g{c->meta.as<StructMeta>(), b->atom_offset, b->positions, c->cnt_structs, c->cnt_atoms,
+    GraphLaunch g{c->meta.as<StructMeta>(), c->atom_struct.as<int32_t>(), b->atom_offset, b->positions,
+                  c->cnt_structs, c->cnt_atoms,
                   c->cnt_rc * c->cnt_rc, c->cnt_eps, c->cnt_k};
     const double E = (double)c->cnt_edges, A = (double)c->cnt_atoms;
     const double rbf_bytes = rs.dtype == DGN_F32 ? 4.0 : (rs.dtype == DGN_F64 ? 8.0 : 0.0);
-    const double bytes = A * 24 + (double)c->cnt_structs * 72 + 8 * (A + 1) + 4 * A + E * (4 + (dist ? 8 : 0)) +
-                         (disp ? 24 * E : 0) + (rbf ? E * rs.nbins * rbf_bytes : 0);
+    const double out_bytes = 8 * (A + 1) + E * (4 + (dist ? 8 : 0)) + (disp ? 24 * E : 0) +
+                             (rbf ? E * rs.nbins * rbf_bytes : 0);
+    if (c->cnt_rows) {
+        // compulsory traffic of the streaming emit: counts + stored rows in, CSR + features out
+        // (+ both endpoint positions for displacements)
+        const double bytes = 4 * A + 16 * E + out_bytes + (disp ? 48 * E : 0);
+        TimedLaunch t(c, betti ? "betti_nl_emit" : "graph_emit", bytes, 0);
+        HIP_TRY(c, launch_graph_emit_rows(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
+                                          c->rows_d.as<uint64_t>(), c->rows_j.as<uint64_t>(),
+                                          const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs));
+        return DGN_OK;
+    }
+    // recompute path: positions + lattice in, counts in, CSR + features out
+    const double bytes = A * 24 + (double)c->cnt_structs * 72 + 4 * A + out_bytes;
     {
         TimedLaunch t(c, betti ? "betti_nl_emit" : "graph_emit", bytes, 0);
         HIP_TRY(c, launch_graph_emit(c->stream, g, cap, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
@@ -417,7 +446,7 @@ void dgn_ctx_destroy(dgn_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     fold_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
+    for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->block_aux, &c->atom_struct, &c->rows_d, &c->rows_j, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
                       &c->b_disp, &c->b_scratch, &c->b_list, &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
         b->release();
     if (c->host_scalars) (void)hipHostFree(c->host_scalars);

@@ -9,11 +9,15 @@
 namespace dgn {
 
 constexpr int kGraphBlock = 256;          // 4 waves
-constexpr int kAtomsPerBlock = 16;        // 4 query atoms per wave, processed in turn
+constexpr int kQA = 64;                   // query atoms per block (16 per wave, round-robin)
+constexpr int kStage = 512;               // structures up to this size are staged in LDS
+constexpr int kRowsMaxK = 64;             // max_neighbors up to this use the stored-rows path
+constexpr int kRowsCap = 128;             // candidates per atom the count pass can rank
 constexpr int kScanThreads = 1024;
 
 struct GraphLaunch {
     const StructMeta* meta;
+    const int32_t* atom_struct;  // [A] structure of each atom (map_atoms_kernel)
     const int64_t* atom_offset;
     const double* pos;
     int64_t num_structures, num_atoms;
@@ -25,13 +29,24 @@ struct RbfSpec {
     int32_t dtype;  // DGN_NONE / DGN_F32 / DGN_F64
     int32_t nbins;
     double dr, inv_sigma2, norm;
+    float inv_nbins, norm_f;
 };
 
+// also fills atom_struct[A] (structure index of every atom)
 hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset,
-                                  int64_t num_structures, double rc, StructMeta* meta);
+                                  int64_t num_structures, double rc, StructMeta* meta, int32_t* atom_struct);
+// per-atom kept counts; per block: block_sums[b] and block_aux[2b] = max candidates,
+// block_aux[2b+1] = sum over atoms of (candidates + 1)^2
+// rows_d/rows_j (optional, [A][max_neighbors]): the ranked kept rows (stored-rows path)
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint32_t* max_candidates, unsigned long long* sum_sq);
-hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, int64_t nblocks, int64_t* total);
+                              uint64_t* block_aux, uint64_t* rows_d, uint64_t* rows_j);
+// streaming emit from stored rows (requires max candidates <= kRowsCap)
+hipError_t launch_graph_emit_rows(hipStream_t s, const GraphLaunch& g, const int32_t* counts,
+                                  const int64_t* block_offsets, const uint64_t* rows_d, const uint64_t* rows_j,
+                                  int64_t* row_ptr, int32_t* col, double* dist, double* disp, void* rbf,
+                                  const RbfSpec& rs);
+hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t* block_aux, int64_t nblocks,
+                             int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq);
 // cap: candidate capacity per query atom (>= max candidates from the count pass)
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
@@ -39,7 +54,7 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const
 
 hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out);
 
-inline int64_t graph_blocks(int64_t num_atoms) { return (num_atoms + kAtomsPerBlock - 1) / kAtomsPerBlock; }
+inline int64_t graph_blocks(int64_t num_atoms) { return (num_atoms + kQA - 1) / kQA; }
 int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
 
 // ---- Betti ----

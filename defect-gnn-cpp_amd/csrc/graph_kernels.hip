@@ -25,7 +25,7 @@
 namespace dgn {
 
 // ------------------------------------------------------------------------------------------
-// Structure metadata
+// Structure metadata + atom -> structure map
 // ------------------------------------------------------------------------------------------
 __global__ void prep_structures_kernel(const double* __restrict__ lattice, const int64_t* __restrict__ atom_offset,
                                        int64_t B, double rc, StructMeta* __restrict__ meta) {
@@ -58,38 +58,93 @@ __global__ void prep_structures_kernel(const double* __restrict__ lattice, const
     meta[b] = m;
 }
 
-// structure containing global atom gi (atom_offset is non-decreasing)
-__device__ __forceinline__ int64_t find_structure(const int64_t* __restrict__ off, int64_t B, int64_t gi) {
-    int64_t lo = 0, hi = B - 1;
-    while (lo < hi) {
-        int64_t mid = (lo + hi + 1) >> 1;
-        if (off[mid] <= gi) lo = mid;
-        else hi = mid - 1;
+// one block per structure: atom_struct[first .. first + natoms) = b
+__global__ __launch_bounds__(256) void map_atoms_kernel(const int64_t* __restrict__ atom_offset,
+                                                        int32_t* __restrict__ atom_struct) {
+    const int64_t b = blockIdx.x;
+    const int64_t a0 = atom_offset[b], a1 = atom_offset[b + 1];
+    for (int64_t a = a0 + threadIdx.x; a < a1; a += blockDim.x) atom_struct[a] = (int32_t)b;
+}
+
+// ------------------------------------------------------------------------------------------
+// Block traversal shared by count and emit: a block owns query atoms [g0, g0 + kQA); it walks
+// the structures those atoms belong to, stages each structure's positions in LDS (SoA, when it
+// has at most kStage atoms; larger ones are read from global/L2), and hands every query atom
+// to one wave (atoms round-robin over the 4 waves).
+// ------------------------------------------------------------------------------------------
+struct StagedPos {
+    double x[kStage], y[kStage], z[kStage];
+};
+
+struct PosSrc {
+    const StagedPos* lds;     // null -> global
+    const double* gpos;       // positions of the structure's first atom
+    __device__ __forceinline__ void get(int j, double p[3]) const {
+        if (lds) {
+            p[0] = lds->x[j];
+            p[1] = lds->y[j];
+            p[2] = lds->z[j];
+        } else {
+            p[0] = gpos[3 * j];
+            p[1] = gpos[3 * j + 1];
+            p[2] = gpos[3 * j + 2];
+        }
     }
-    return lo;
+};
+
+__device__ __forceinline__ int32_t uni_i32(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <class PerAtom>
+__device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, StagedPos& st, PerAtom&& per_atom) {
+    const int w = threadIdx.x / kWave;
+    const int64_t g0 = (int64_t)blockIdx.x * kQA;
+    const int64_t g1 = g0 + kQA < g.num_atoms ? g0 + kQA : g.num_atoms;
+    const int32_t b_first = uni_i32(g.atom_struct[g0]);
+    const int32_t b_last = uni_i32(g.atom_struct[g1 - 1]);
+    for (int32_t b = b_first; b <= b_last; ++b) {
+        const StructMeta& M = g.meta[b];
+        const int64_t first = M.first;
+        const int natoms = M.natoms;
+        if (natoms == 0) continue;
+        const bool staged = natoms <= kStage;
+        if (staged) {
+            __syncthreads();  // previous segment done with the stage
+            const double* src = g.pos + 3 * first;
+            for (int t = threadIdx.x; t < natoms; t += kGraphBlock) {
+                st.x[t] = src[3 * t];
+                st.y[t] = src[3 * t + 1];
+                st.z[t] = src[3 * t + 2];
+            }
+            __syncthreads();
+        }
+        const PosSrc P{staged ? &st : nullptr, g.pos + 3 * first};
+        const int64_t s0 = g0 > first ? g0 : first;
+        const int64_t s1 = g1 < first + natoms ? g1 : first + natoms;
+        for (int64_t gi = s0 + w; gi < s1; gi += kGraphBlock / kWave) per_atom(M, P, gi, (int)(gi - g0));
+    }
 }
 
 // ------------------------------------------------------------------------------------------
 // Candidate enumeration: all (j, image) with d2 < rc^2 around query atom q (wave-uniform call).
-// visit(hit, j, na, nb, nc, d, p) is invoked by every lane once per step (hit false = idle).
+// Lane j enumerates only the images whose fractional slab can reach rc, clamped to the
+// reference's +-nref range, with nested counters (no integer division).
+// visit(hit, j, na, nb, nc, d) is invoked by every lane once per step (hit false = idle).
 // ------------------------------------------------------------------------------------------
 template <class Visit>
-__device__ __forceinline__ void for_each_candidate(const StructMeta& M, const double* __restrict__ pos,
-                                                   const double q[3], int li, double rc2, double eps,
-                                                   Visit&& visit) {
+__device__ __forceinline__ void for_each_candidate(const StructMeta& M, const PosSrc& P, const double q[3], int li,
+                                                   double rc2, double eps, Visit&& visit) {
     const int lane = lane_id();
-    for (int base = 0; base < M.natoms; base += kWave) {
+    const int natoms = M.natoms;
+    for (int base = 0; base < natoms; base += kWave) {
         const int j = base + lane;
         double p[3] = {0.0, 0.0, 0.0};
-        int lo[3] = {0, 0, 0}, ext[3] = {0, 0, 0};
+        int lo[3] = {0, 0, 0}, hi[3] = {-1, -1, -1};
         int ni = 0;
-        if (j < M.natoms) {
-            const double* pj = pos + 3 * (M.first + j);
-            p[0] = pj[0];
-            p[1] = pj[1];
-            p[2] = pj[2];
+        if (j < natoms) {
+            P.get(j, p);
             const double r0 = p[0] - q[0], r1 = p[1] - q[1], r2 = p[2] - q[2];
             ni = 1;
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const double df = r0 * M.R[k] + r1 * M.R[3 + k] + r2 * M.R[6 + k];
                 int l = (int)ceil(-df - M.h[k] - 1e-9);
@@ -97,36 +152,38 @@ __device__ __forceinline__ void for_each_candidate(const StructMeta& M, const do
                 l = l < -M.nref ? -M.nref : l;
                 h = h > M.nref ? M.nref : h;
                 lo[k] = l;
-                ext[k] = h - l + 1;
-                ni = ext[k] > 0 ? ni * ext[k] : 0;
+                hi[k] = h;
+                ni = h >= l ? ni * (h - l + 1) : 0;
             }
         }
-        const int nmax = wave_max(ni);
-        for (int t = 0; t < nmax; ++t) {
+        int na = lo[0], nb = lo[1], nc = lo[2];
+        for (int t = 0; ballot(t < ni); ++t) {
             bool hit = false;
-            int na = 0, nb = 0, nc = 0;
-            double d = 0.0, pk[3] = {0.0, 0.0, 0.0};
+            double d = 0.0;
+            const int ca = na, cb = nb, cc = nc;
             if (t < ni) {
-                const int tc = t % ext[2];
-                const int tt = t / ext[2];
-                nc = lo[2] + tc;
-                nb = lo[1] + tt % ext[1];
-                na = lo[0] + tt / ext[1];
-                const double dna = (double)na, dnb = (double)nb, dnc = (double)nc;
+                const double dna = (double)ca, dnb = (double)cb, dnc = (double)cc;
                 double d2 = 0.0;
+#pragma unroll
                 for (int k = 0; k < 3; ++k) {
                     // offset = (na*a + nb*b) + nc*c (neighbor_list.cpp:82-84); p = pos + offset (:87)
                     const double off = (dna * M.L[k] + dnb * M.L[3 + k]) + dnc * M.L[6 + k];
-                    pk[k] = p[k] + off;
-                    const double diff = q[k] - pk[k];  // L2_Simple_Adaptor: (a - b)^2 accumulated
+                    const double diff = q[k] - (p[k] + off);  // L2_Simple_Adaptor: (a - b)^2 accumulated
                     d2 += diff * diff;
                 }
                 if (d2 < rc2) {  // RadiusResultSet: strict
                     d = sqrt(d2);
                     hit = !(j == li && d < eps);  // self skip (neighbor_list.cpp:47)
                 }
+                if (++nc > hi[2]) {
+                    nc = lo[2];
+                    if (++nb > hi[1]) {
+                        nb = lo[1];
+                        ++na;
+                    }
+                }
             }
-            visit(hit, j, na, nb, nc, d, pk);
+            visit(hit, j, ca, cb, cc, d);
         }
     }
 }
@@ -137,57 +194,130 @@ __device__ __forceinline__ uint64_t pack_jimg(int j, int na, int nb, int nc) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 1: per-atom candidate counts.
+// Ranking of one atom's compacted candidates by (distance, j, image) — the canonical row order
+// (the reference's nanoflann order differs only among exact ties). Lane s ranks entry s by
+// counting smaller keys (broadcast LDS reads); visit(rank, kd, kj) for every entry.
 // ------------------------------------------------------------------------------------------
+template <class Visit>
+__device__ __forceinline__ void rank_candidates(const uint64_t* kd_, const uint64_t* kj_, int m, Visit&& visit) {
+    for (int s = lane_id(); s < m; s += kWave) {
+        const uint64_t kd = kd_[s], kj = kj_[s];
+        int rank = 0;
+        for (int u = 0; u < m; ++u) {
+            const uint64_t ud = kd_[u], uj = kj_[u];
+            rank += (ud < kd) | ((ud == kd) & (uj < kj));
+        }
+        visit(rank, kd, kj);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 1: per-atom kept counts + per-block (sum, max candidates, sum (m+1)^2). No atomics.
+// ROWS: also rank each atom's candidates and store its kept rows (distance bits, packed
+// j/image) at rows[gi * K + rank], K = max_neighbors <= kRowsMaxK, so the emit pass only
+// streams; atoms with more than kRowsCap candidates set the block's overflow bit instead.
+// ------------------------------------------------------------------------------------------
+template <bool ROWS>
 __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
                                                                    int64_t* __restrict__ block_sums,
-                                                                   uint32_t* __restrict__ max_candidates,
-                                                                   unsigned long long* __restrict__ sum_sq) {
-    __shared__ int64_t wsum[kGraphBlock / kWave];
+                                                                   uint64_t* __restrict__ block_aux,
+                                                                   uint64_t* __restrict__ rows_d,
+                                                                   uint64_t* __restrict__ rows_j) {
+    constexpr int W = kGraphBlock / kWave;
+    constexpr int CAP = ROWS ? kRowsCap : 1;
+    __shared__ StagedPos st;
+    __shared__ int64_t wsum[W];
+    __shared__ uint64_t wmax[W], wsq[W];
+    __shared__ uint64_t key_d[W][CAP];
+    __shared__ uint64_t key_j[W][CAP];
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
     int64_t my_sum = 0;
     uint32_t my_max = 0;
-    unsigned long long my_sq = 0;
-    for (int t = w; t < kAtomsPerBlock; t += kGraphBlock / kWave) {
-        const int64_t gi = (int64_t)blockIdx.x * kAtomsPerBlock + t;
-        if (gi >= g.num_atoms) break;
-        const int64_t b = find_structure(g.atom_offset, g.num_structures, gi);
-        const StructMeta M = g.meta[b];
-        const double q[3] = {g.pos[3 * gi], g.pos[3 * gi + 1], g.pos[3 * gi + 2]};
+    uint64_t my_sq = 0;
+    for_block_atoms(g, st, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int) {
+        const int li = (int)(gi - M.first);
+        double q[3];
+        P.get(li, q);
         int m = 0;
-        for_each_candidate(M, g.pos, q, (int)(gi - M.first), g.rc2, g.eps,
-                           [&](bool hit, int, int, int, int, double, const double*) { m += __popcll(ballot(hit)); });
+        if constexpr (ROWS) {
+            for_each_candidate(M, P, q, li, g.rc2, g.eps, [&](bool hit, int j, int na, int nb, int nc, double d) {
+                const uint64_t bal = ballot(hit);
+                if (hit) {
+                    const int slot = m + mask_prefix(bal);
+                    if (slot < CAP) {
+                        key_d[w][slot] = f64_bits(d);
+                        key_j[w][slot] = pack_jimg(j, na, nb, nc);
+                    }
+                }
+                m += __popcll(bal);
+            });
+        } else {
+            for_each_candidate(M, P, q, li, g.rc2, g.eps,
+                               [&](bool hit, int, int, int, int, double) { m += __popcll(ballot(hit)); });
+        }
         const int64_t c = (uint64_t)m < g.kmax ? (int64_t)m : (int64_t)g.kmax;
         if (lane == 0) counts[gi] = (int32_t)c;
+        if constexpr (ROWS) {
+            if (m <= CAP) {
+                __builtin_amdgcn_wave_barrier();
+                const int64_t base = gi * (int64_t)g.kmax;
+                rank_candidates(key_d[w], key_j[w], m, [&](int rank, uint64_t kd, uint64_t kj) {
+                    if (rank < c) {
+                        rows_d[base + rank] = kd;
+                        rows_j[base + rank] = kj;
+                    }
+                });
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
         my_sum += c;
         my_max = (uint32_t)m > my_max ? (uint32_t)m : my_max;
-        my_sq += (unsigned long long)(m + 1) * (unsigned long long)(m + 1);  // local-complex n^2
+        my_sq += (uint64_t)(m + 1) * (uint64_t)(m + 1);  // local-complex n^2
+    });
+    if (lane == 0) {
+        wsum[w] = my_sum;
+        wmax[w] = my_max;
+        wsq[w] = my_sq;
     }
-    if (lane == 0) wsum[w] = my_sum;
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t s = 0;
-        for (int k = 0; k < kGraphBlock / kWave; ++k) s += wsum[k];
+        uint64_t mx = 0, sq = 0;
+        for (int k = 0; k < W; ++k) {
+            s += wsum[k];
+            mx = wmax[k] > mx ? wmax[k] : mx;
+            sq += wsq[k];
+        }
         block_sums[blockIdx.x] = s;
+        block_aux[2 * blockIdx.x] = mx;
+        block_aux[2 * blockIdx.x + 1] = sq;
     }
-    if (lane == 0 && my_max) atomicMax(max_candidates, my_max);
-    if (lane == 0 && my_sq) atomicAdd(sum_sq, my_sq);
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 2: exclusive scan of the per-block sums (one workgroup), total -> *total.
+// Kernel 2: exclusive scan of the per-block sums (one workgroup) -> *total, and the max /
+// sum reductions of block_aux -> *max_candidates, *sum_sq.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __restrict__ v, int64_t n,
-                                                                  int64_t* __restrict__ total) {
+__global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __restrict__ v,
+                                                                  const uint64_t* __restrict__ aux, int64_t n,
+                                                                  int64_t* __restrict__ total,
+                                                                  uint32_t* __restrict__ max_candidates,
+                                                                  unsigned long long* __restrict__ sum_sq) {
     __shared__ int64_t wtot[kScanThreads / kWave];
+    __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave];
     __shared__ int64_t carry_s;
     const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
     if (tid == 0) carry_s = 0;
+    uint64_t mx = 0, sq = 0;
     __syncthreads();
     for (int64_t base = 0; base < n; base += kScanThreads) {
         const int64_t i = base + tid;
         const int64_t x = i < n ? v[i] : 0;
+        if (i < n) {
+            mx = aux[2 * i] > mx ? aux[2 * i] : mx;
+            sq += aux[2 * i + 1];
+        }
         const int64_t inc = wave_inclusive_sum(x);
         if (lane == kWave - 1) wtot[w] = inc;
         __syncthreads();
@@ -199,7 +329,23 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
         if (tid == kScanThreads - 1) carry_s = carry + woff + inc;
         __syncthreads();
     }
-    if (tid == 0) *total = carry_s;
+    mx = wave_max(mx);
+    sq = wave_sum(sq);
+    if (lane == 0) {
+        wmx[w] = mx;
+        wsq[w] = sq;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        *total = carry_s;
+        uint64_t m = 0, s = 0;
+        for (int k = 0; k < kScanThreads / kWave; ++k) {
+            m = wmx[k] > m ? wmx[k] : m;
+            s += wsq[k];
+        }
+        *max_candidates = (uint32_t)m;
+        *sum_sq = s;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -220,6 +366,51 @@ __device__ __forceinline__ double rbf_value_f64(double d, int k, const RbfSpec& 
     return r.norm * exp(-0.5 * (t * t) * r.inv_sigma2);
 }
 
+// flat element f of an atom's RBF block -> (edge, bin); exact for f < 2^24
+__device__ __forceinline__ void rbf_split(int f, const RbfSpec& r, int& e, int& k) {
+    e = (int)((float)f * r.inv_nbins);
+    if (e * r.nbins > f) --e;
+    else if ((e + 1) * r.nbins <= f) ++e;
+    k = f - e * r.nbins;
+}
+
+// write the kept x nbins RBF block of one atom: scalar head to a 16-byte boundary, 16-byte
+// vector body, scalar tail (all lanes of the wave, coalesced)
+template <typename T>
+__device__ __forceinline__ void write_rbf_block(T* __restrict__ out, int total, const double* sd, const RbfSpec& rs) {
+    constexpr int V = 16 / sizeof(T);
+    const int lane = lane_id();
+    const int mis = (int)(((uintptr_t)out / sizeof(T)) & (V - 1));
+    int head = mis ? V - mis : 0;
+    head = head < total ? head : total;
+    auto val = [&](int f) -> T {
+        int e, k;
+        rbf_split(f, rs, e, k);
+        if constexpr (sizeof(T) == 4) return rbf_value_f32(sd[e], k, rs);
+        else return rbf_value_f64(sd[e], k, rs);
+    };
+    if (lane < head) out[lane] = val(lane);
+    const int nvec = (total - head) / V;
+    for (int v = lane; v < nvec; v += kWave) {
+        const int f = head + V * v;
+        if constexpr (sizeof(T) == 4) {
+            float4 o;
+            o.x = val(f);
+            o.y = val(f + 1);
+            o.z = val(f + 2);
+            o.w = val(f + 3);
+            *reinterpret_cast<float4*>(out + f) = o;
+        } else {
+            double2 o;
+            o.x = val(f);
+            o.y = val(f + 1);
+            *reinterpret_cast<double2*>(out + f) = o;
+        }
+    }
+    const int tail0 = head + V * nvec;
+    if (tail0 + lane < total) out[tail0 + lane] = val(tail0 + lane);
+}
+
 template <int CAP>
 __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, const int32_t* __restrict__ counts,
                                                                   const int64_t* __restrict__ block_offsets,
@@ -228,67 +419,55 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                                                                   double* __restrict__ disp, void* __restrict__ rbf,
                                                                   RbfSpec rs, uint32_t* __restrict__ error_flag) {
     constexpr int W = kGraphBlock / kWave;
+    __shared__ StagedPos st;
     __shared__ uint64_t key_d[W][CAP];
     __shared__ uint64_t key_j[W][CAP];
     __shared__ double sorted_d[W][CAP];
-    __shared__ int64_t row_start[kAtomsPerBlock];
+    __shared__ int64_t row_start[kQA];
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int64_t first_atom = (int64_t)blockIdx.x * kAtomsPerBlock;
+    const int64_t g0 = (int64_t)blockIdx.x * kQA;
 
-    // local scan of this block's counts -> row starts (and row_ptr)
+    // local scan of this block's counts -> row starts (and row_ptr); kQA == one wave
     if (w == 0) {
-        const int64_t gi = first_atom + lane;
-        const int64_t c = (lane < kAtomsPerBlock && gi < g.num_atoms) ? counts[gi] : 0;
+        const int64_t gi = g0 + lane;
+        const int64_t c = gi < g.num_atoms ? counts[gi] : 0;
         const int64_t inc = wave_inclusive_sum(c);
         const int64_t start = block_offsets[blockIdx.x] + inc - c;
-        if (lane < kAtomsPerBlock) row_start[lane] = start;
-        if (lane < kAtomsPerBlock && gi < g.num_atoms) {
+        row_start[lane] = start;
+        if (gi < g.num_atoms) {
             row_ptr[gi] = start;
             if (gi == g.num_atoms - 1) row_ptr[g.num_atoms] = start + c;
         }
     }
     __syncthreads();
-
-    for (int t = w; t < kAtomsPerBlock; t += W) {
-        const int64_t gi = first_atom + t;
-        if (gi >= g.num_atoms) break;
-        const int64_t b = find_structure(g.atom_offset, g.num_structures, gi);
-        const StructMeta M = g.meta[b];
-        const double q[3] = {g.pos[3 * gi], g.pos[3 * gi + 1], g.pos[3 * gi + 2]};
+    for_block_atoms(g, st, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t) {
         const int li = (int)(gi - M.first);
-        // 1. compact hits into the LDS candidate list
+        double q[3];
+        P.get(li, q);
+        // 1. compact hits into the wave's LDS candidate list
         int m = 0;
-        bool overflow = false;
-        for_each_candidate(M, g.pos, q, li, g.rc2, g.eps,
-                           [&](bool hit, int j, int na, int nb, int nc, double d, const double*) {
-                               const uint64_t bal = ballot(hit);
-                               if (hit) {
-                                   const int slot = m + mask_prefix(bal);
-                                   if (slot < CAP) {
-                                       key_d[w][slot] = f64_bits(d);
-                                       key_j[w][slot] = pack_jimg(j, na, nb, nc);
-                                   }
-                               }
-                               m += __popcll(bal);
-                           });
-        if (m > CAP) overflow = true;
+        for_each_candidate(M, P, q, li, g.rc2, g.eps, [&](bool hit, int j, int na, int nb, int nc, double d) {
+            const uint64_t bal = ballot(hit);
+            if (hit) {
+                const int slot = m + mask_prefix(bal);
+                if (slot < CAP) {
+                    key_d[w][slot] = f64_bits(d);
+                    key_j[w][slot] = pack_jimg(j, na, nb, nc);
+                }
+            }
+            m += __popcll(bal);
+        });
         const int cnt = counts[gi];
         const int64_t rs0 = row_start[t];
         const int kept = (uint64_t)m < g.kmax ? m : (int)g.kmax;
-        if (overflow || kept != cnt) {
-            if (lane == 0) atomicOr(error_flag, overflow ? 1u : 2u);
-            continue;
+        if (m > CAP || kept != cnt) {
+            if (lane == 0) atomicOr(error_flag, m > CAP ? 1u : 2u);
+            return;
         }
         __builtin_amdgcn_wave_barrier();
         // 2. rank by (distance, j, image) and write the kept rows
-        for (int s = lane; s < m; s += kWave) {
-            const uint64_t kd = key_d[w][s], kj = key_j[w][s];
-            int rank = 0;
-            for (int u = 0; u < m; ++u) {
-                const uint64_t ud = key_d[w][u], uj = key_j[w][u];
-                rank += (ud < kd) | ((ud == kd) & (uj < kj));
-            }
+        rank_candidates(key_d[w], key_j[w], m, [&](int rank, uint64_t kd, uint64_t kj) {
             if (rank < kept) {
                 const int64_t e = rs0 + rank;
                 const int j = (int)(kj >> 24);
@@ -299,33 +478,162 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 if (disp) {
                     const int na = (int)((kj >> 16) & 255) - 128, nb = (int)((kj >> 8) & 255) - 128,
                               nc = (int)(kj & 255) - 128;
-                    const double* pj = g.pos + 3 * (M.first + j);
+                    double pj[3];
+                    P.get(j, pj);
                     for (int k = 0; k < 3; ++k) {
                         const double off = ((double)na * M.L[k] + (double)nb * M.L[3 + k]) + (double)nc * M.L[6 + k];
                         disp[3 * e + k] = (pj[k] + off) - q[k];  // delta_r = p - q (neighbor_list.cpp:51)
                     }
                 }
             }
-        }
+        });
         __builtin_amdgcn_wave_barrier();
         // 3. RBF block: kept x nbins contiguous values starting at rs0 * nbins
         if (rs.dtype != 0 && rbf) {
             const int total = kept * rs.nbins;
-            if (rs.dtype == 1) {
-                float* out = reinterpret_cast<float*>(rbf) + rs0 * rs.nbins;
-                for (int f = lane; f < total; f += kWave) {
-                    const int e = f / rs.nbins, k = f - e * rs.nbins;
-                    out[f] = rbf_value_f32(sorted_d[w][e], k, rs);
-                }
-            } else {
-                double* out = reinterpret_cast<double*>(rbf) + rs0 * rs.nbins;
-                for (int f = lane; f < total; f += kWave) {
-                    const int e = f / rs.nbins, k = f - e * rs.nbins;
-                    out[f] = rbf_value_f64(sorted_d[w][e], k, rs);
-                }
-            }
+            if (rs.dtype == 1) write_rbf_block(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, sorted_d[w], rs);
+            else write_rbf_block(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sorted_d[w], rs);
         }
         __builtin_amdgcn_wave_barrier();
+    });
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 3b: streaming emit from the rows the count pass stored (ROWS mode). A block covers
+// kQA atoms, whose edges and RBF rows are contiguous in the CSR: phase 1 places the kept rows
+// (col, dist, displacement) edge-parallel and keeps the distances in LDS; phase 2 writes the
+// block's whole RBF region as one flat stream of 16-byte stores.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rbf_value_f32_fast(double d, int k, const RbfSpec& r) {
+    const double t = (double)k * r.dr - d;  // center - distance (edge_features.cpp:20-21)
+    const double x = ((-0.5 * (t * t)) * r.inv_sigma2) * 1.4426950408889634074;
+    const double n = rint(x);
+    const float e = __builtin_amdgcn_exp2f((float)(x - n));  // |x - n| <= 0.5
+    return __builtin_ldexpf(e, (int)n) * r.norm_f;
+}
+
+__global__ __launch_bounds__(kGraphBlock) void graph_emit_rows_kernel(
+    GraphLaunch g, const int32_t* __restrict__ counts, const int64_t* __restrict__ block_offsets,
+    const uint64_t* __restrict__ rows_d, const uint64_t* __restrict__ rows_j, int64_t* __restrict__ row_ptr,
+    int32_t* __restrict__ col, double* __restrict__ dist, double* __restrict__ disp, void* __restrict__ rbf,
+    RbfSpec rs) {
+    extern __shared__ double dl[];  // [kQA * K] distances of the block's edges, CSR order
+    __shared__ int64_t row_start[kQA + 1];
+    __shared__ int32_t cnt[kQA];
+    const int tid = threadIdx.x, lane = lane_id();
+    const int64_t g0 = (int64_t)blockIdx.x * kQA;
+    const int K = (int)g.kmax;
+    if (tid < kWave) {
+        const int64_t gi = g0 + lane;
+        const int64_t c = gi < g.num_atoms ? counts[gi] : 0;
+        const int64_t inc = wave_inclusive_sum(c);
+        const int64_t start = block_offsets[blockIdx.x] + inc - c;
+        row_start[lane] = start;
+        cnt[lane] = (int32_t)c;
+        if (lane == kWave - 1) row_start[kQA] = start + c;
+        if (gi < g.num_atoms) {
+            row_ptr[gi] = start;
+            if (gi == g.num_atoms - 1) row_ptr[g.num_atoms] = start + c;
+        }
+    }
+    __syncthreads();
+    const int64_t e0 = row_start[0];
+    // phase 1: slot p = (atom a, rank r), r < K; stored rows are read in order (coalesced)
+    const float invK = 1.0f / (float)K;
+    for (int p = tid; p < kQA * K; p += kGraphBlock) {
+        int a = (int)((float)p * invK);
+        if (a * K > p) --a;
+        else if ((a + 1) * K <= p) ++a;
+        const int r = p - a * K;
+        const int64_t gi = g0 + a;
+        if (gi >= g.num_atoms || r >= cnt[a]) continue;
+        const uint64_t kd = rows_d[gi * K + r], kj = rows_j[gi * K + r];
+        const int64_t e = row_start[a] + r;
+        const double d = __longlong_as_double((long long)kd);
+        const int j = (int)(kj >> 24);
+        col[e] = j;
+        if (dist) dist[e] = d;
+        dl[e - e0] = d;
+        if (disp) {
+            const StructMeta& M = g.meta[g.atom_struct[gi]];
+            const int na = (int)((kj >> 16) & 255) - 128, nb = (int)((kj >> 8) & 255) - 128, nc = (int)(kj & 255) - 128;
+            const double* pj = g.pos + 3 * (M.first + j);
+            const double* q = g.pos + 3 * gi;
+            for (int k = 0; k < 3; ++k) {
+                const double off = ((double)na * M.L[k] + (double)nb * M.L[3 + k]) + (double)nc * M.L[6 + k];
+                disp[3 * e + k] = (pj[k] + off) - q[k];  // delta_r = p - q (neighbor_list.cpp:51)
+            }
+        }
+    }
+    if (rs.dtype == 0 || !rbf) return;
+    __syncthreads();
+    // phase 2: the block's RBF region [e0 * nb, e1 * nb) as one flat stream
+    const int nb = rs.nbins;
+    const int total = (int)(row_start[kQA] - e0) * nb;
+    auto split = [&](int f, int& le, int& k) {
+        le = (int)((float)f * rs.inv_nbins);
+        if (le * nb > f) --le;
+        else if ((le + 1) * nb <= f) ++le;
+        k = f - le * nb;
+    };
+    if (rs.dtype == 1) {
+        float* out = reinterpret_cast<float*>(rbf) + e0 * nb;
+        const int mis = (int)(((uintptr_t)out >> 2) & 3);
+        int head = mis ? 4 - mis : 0;
+        head = head < total ? head : total;
+        if (tid < head) {
+            int le, k;
+            split(tid, le, k);
+            out[tid] = rbf_value_f32_fast(dl[le], k, rs);
+        }
+        const int nvec = (total - head) >> 2;
+        for (int v = tid; v < nvec; v += kGraphBlock) {
+            const int f = head + 4 * v;
+            int le, k;
+            split(f, le, k);
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                o[u] = rbf_value_f32_fast(dl[le], k, rs);
+                if (++k == nb) {
+                    k = 0;
+                    ++le;
+                }
+            }
+            *reinterpret_cast<float4*>(out + f) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        const int t0 = head + 4 * nvec;
+        if (t0 + tid < total) {
+            int le, k;
+            split(t0 + tid, le, k);
+            out[t0 + tid] = rbf_value_f32_fast(dl[le], k, rs);
+        }
+    } else {
+        double* out = reinterpret_cast<double*>(rbf) + e0 * nb;
+        const int head = ((((uintptr_t)out >> 3) & 1) && total > 0) ? 1 : 0;
+        if (tid < head) out[0] = rbf_value_f64(dl[0], 0, rs);
+        const int nvec = (total - head) >> 1;
+        for (int v = tid; v < nvec; v += kGraphBlock) {
+            const int f = head + 2 * v;
+            int le, k;
+            split(f, le, k);
+            double o[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                o[u] = rbf_value_f64(dl[le], k, rs);
+                if (++k == nb) {
+                    k = 0;
+                    ++le;
+                }
+            }
+            *reinterpret_cast<double2*>(out + f) = make_double2(o[0], o[1]);
+        }
+        const int t0 = head + 2 * nvec;
+        if (t0 + tid < total) {
+            int le, k;
+            split(t0 + tid, le, k);
+            out[t0 + tid] = rbf_value_f64(dl[le], k, rs);
+        }
     }
 }
 
@@ -364,25 +672,44 @@ hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& 
 // host launchers
 // ------------------------------------------------------------------------------------------
 hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset, int64_t B,
-                                  double rc, StructMeta* meta) {
+                                  double rc, StructMeta* meta, int32_t* atom_struct) {
     if (B <= 0) return hipSuccess;
     const int t = 128;
     hipLaunchKernelGGL(prep_structures_kernel, dim3((unsigned)((B + t - 1) / t)), dim3(t), 0, s, lattice, atom_offset,
                        B, rc, meta);
+    hipLaunchKernelGGL(map_atoms_kernel, dim3((unsigned)B), dim3(256), 0, s, atom_offset, atom_struct);
     return hipGetLastError();
 }
 
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint32_t* max_candidates, unsigned long long* sum_sq) {
+                              uint64_t* block_aux, uint64_t* rows_d, uint64_t* rows_j) {
     const int64_t nb = graph_blocks(g.num_atoms);
     if (nb <= 0) return hipSuccess;
-    hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
-                       max_candidates, sum_sq);
+    if (rows_d)
+        hipLaunchKernelGGL(graph_count_kernel<true>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts,
+                           block_sums, block_aux, rows_d, rows_j);
+    else
+        hipLaunchKernelGGL(graph_count_kernel<false>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts,
+                           block_sums, block_aux, rows_d, rows_j);
     return hipGetLastError();
 }
 
-hipError_t launch_block_scan(hipStream_t s, int64_t* v, int64_t n, int64_t* total) {
-    hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, v, n, total);
+hipError_t launch_graph_emit_rows(hipStream_t s, const GraphLaunch& g, const int32_t* counts,
+                                  const int64_t* block_offsets, const uint64_t* rows_d, const uint64_t* rows_j,
+                                  int64_t* row_ptr, int32_t* col, double* dist, double* disp, void* rbf,
+                                  const RbfSpec& rs) {
+    const int64_t nb = graph_blocks(g.num_atoms);
+    if (nb <= 0) return hipSuccess;
+    const size_t shmem = sizeof(double) * (size_t)kQA * (size_t)g.kmax;
+    hipLaunchKernelGGL(graph_emit_rows_kernel, dim3((unsigned)nb), dim3(kGraphBlock), shmem, s, g, counts,
+                       block_offsets, rows_d, rows_j, row_ptr, col, dist, disp, rbf, rs);
+    return hipGetLastError();
+}
+
+hipError_t launch_block_scan(hipStream_t s, int64_t* v, const uint64_t* aux, int64_t n, int64_t* total,
+                             uint32_t* max_candidates, unsigned long long* sum_sq) {
+    hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, v, aux, n, total, max_candidates,
+                       sum_sq);
     return hipGetLastError();
 }
 

@@ -91,24 +91,33 @@ def test_supercell_4096(ctx):
     assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
 
 
-def test_empty_and_ragged(ctx):
-    # structures of different sizes in one batch, including a 1-atom cell with no neighbours
+@pytest.mark.parametrize("k,rbf_rc,dtype", [(None, 5.0, dgn.DGN_F32), (7, 4.95, dgn.DGN_F64), (20, 4.95, dgn.DGN_F32)])
+def test_empty_and_ragged(ctx, k, rbf_rc, dtype):
+    # structures of different sizes in one batch, including a 1-atom cell with no neighbours and
+    # an empty structure; odd RBF bin counts exercise the unaligned head/tail of the RBF stream
     a = dgn.synth_batch("sc", 2, 1)
     b = dgn.synth_batch("fcc", 2, 1)
+    c = dgn.synth_batch("sc", 3, 2)
     lone = {"lattice": np.eye(3)[None] * 20.0, "positions": np.array([[1.0, 2.0, 3.0]]),
             "species": np.zeros(1, np.int32)}
-    parts = [a, lone, b]
+    empty = {"lattice": np.eye(3)[None] * 10.0, "positions": np.zeros((0, 3)), "species": np.zeros(0, np.int32)}
+    parts = [a, lone, empty, b, c]
     batch = {"lattice": np.concatenate([x["lattice"] for x in parts]),
              "positions": np.concatenate([x["positions"] for x in parts]),
              "species": np.concatenate([x["species"] for x in parts]).astype(np.int32)}
     sizes = [len(x["positions"]) for x in parts]
     batch["atom_offset"] = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    p = abi.graph_params(r_cutoff=5.0, max_neighbors=None, rbf_cutoff=5.0, rbf_dr=0.1)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=k, rbf_cutoff=rbf_rc, rbf_dr=0.1, rbf_dtype=dtype,
+                         write_displacement=True)
     g = ctx.host_graph(batch, p)
-    rp, col, dist, _ = oracle_batch_csr(batch, 5.0, None)
+    rp, col, dist, disp = oracle_batch_csr(batch, 5.0, k)
     assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
     lone_row = sizes[0]
     assert rp[lone_row + 1] - rp[lone_row] == 0
+    ref = np.stack([O.gaussian_rbf(d, rbf_rc, 0.1) for d in dist])
+    assert g["rbf"].shape == ref.shape
+    np.testing.assert_allclose(g["rbf"], ref, rtol=1e-13 if dtype == dgn.DGN_F64 else RBF_RTOL, atol=0)
 
 
 @pytest.mark.parametrize("layout", [0, 1])
