@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--dr", type=float, default=0.1)
     ap.add_argument("--betti-rc", type=float, default=5.0)
     ap.add_argument("--no-betti", action="store_true", help="graph only (config 2 style)")
-    ap.add_argument("--cpu-sample", type=int, default=16, help="structures in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=128, help="structures in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),

@@ -51,8 +51,8 @@ def main():
     fetch = find(os.path.join(a.dir, "fetch"), "*counter_collection.csv")
     write = find(os.path.join(a.dir, "write"), "*counter_collection.csv")
     if fetch and write:
-        fv = pmc_per_launch(fetch, "graph_emit_kernel", "FETCH_SIZE")
-        wv = pmc_per_launch(write, "graph_emit_kernel", "WRITE_SIZE")
+        fv = pmc_per_launch(fetch, "graph_emit", "FETCH_SIZE")
+        wv = pmc_per_launch(write, "graph_emit", "WRITE_SIZE")
         if fv and wv:
             f_kb = sum(fv) / len(fv)
             w_kb = sum(wv) / len(wv)
