@@ -46,22 +46,26 @@ $(LIB): $(KOBJS)
 oracle:
 	$(MAKE) -C oracle
 
-# diagnostics variant: per-phase cycle stamps in the Betti kernel (never used by bench/tests)
-DBUILD := $(PKG)/build_diag
-DIAG   := $(PKG)/lib/libdgn_diag.so
+# diagnostics variant: per-phase cycle stamps in the Betti kernel (never used by bench/tests).
+#   make diag [DIAGTAG=x DIAGFLAGS=-DSOMETHING] -> lib/libdgn_diag[_x].so
+DIAGTAG   ?=
+DIAGFLAGS ?=
+DSUF   := $(if $(DIAGTAG),_$(DIAGTAG),)
+DBUILD := $(PKG)/build_diag$(DSUF)
+DIAG   := $(PKG)/lib/libdgn_diag$(DSUF).so
 diag: $(DIAG)
 $(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(DBUILD)
-	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -c $< -o $@
 $(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(DBUILD)
-	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -x hip -c $< -o $@
 $(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/dgn_api.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(DBUILD) $(DIAG) $(FACADE) $(FBIN)
+	rm -rf $(BUILD) $(LIB) $(PKG)/build_diag* $(PKG)/lib/libdgn_diag*.so $(FACADE) $(FBIN)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean diag facade

@@ -32,7 +32,7 @@
 
 namespace dgn {
 
-constexpr int kVCap = 128;        // simplices in one column's V list (LDS)
+constexpr int kVCap = 128;        // simplices in one column's V list (registers: 2 per lane)
 constexpr int kVStoreLds = 128;   // stored V-list entries kept in LDS (rest in scratch)
 constexpr int kNALds = 64;        // sorted non-apparent column records kept in LDS
 constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
@@ -79,7 +79,6 @@ struct BettiSmem {
     uint64_t tree[NP];
     uint16_t edges[NP * (NP - 1) / 2];
     uint32_t cleared[(NP * (NP - 1) * (NP - 2) / 6 + 31) / 32];
-    uint32_t vbits[(NP * (NP - 1) * (NP - 2) / 6 + 31) / 32];  // V membership (edges or triangles)
     union {
         struct {
             double X[NP][3];
@@ -91,7 +90,6 @@ struct BettiSmem {
         } na;
     } u;
     uint32_t vstore[kVStoreLds];
-    uint32_t vcur[kVCap];
     uint64_t piv[kPivLds];
     uint32_t vmeta[kPivLds];
     float d0[NP];
@@ -241,7 +239,6 @@ struct Complex {
     template <typename T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scratch + off); }
     __device__ float2* pairs(int dim) const { return sp<float2>(dim == 1 ? ScratchLayout::p1 : ScratchLayout::p2); }
-    __device__ bool vbit(int idx) const { return (s.vbits[idx >> 5] >> (idx & 31)) & 1u; }
 
     // wave-uniform: append pairs (birth, death) for lanes with `emit`
     __device__ void append_pairs(int dim, bool emit, float birth, float death) {
@@ -254,30 +251,25 @@ struct Complex {
         np += __popcll(bal);
     }
 
-    // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand
+    // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand.
+    // Inserting a larger vertex k gives a larger packed tuple, i.e. an F-smaller key among
+    // cofacets of equal diameter; so walking k downwards, the first k whose distances to the
+    // simplex are all <= diam yields the F-minimal cofacet (diameter diam, largest index)
+    // and ends the search. Cofacets seen before it have larger diameters.
     __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, float diam, uint64_t cand) const {
         uint64_t best = kInf;
         while (cand) {
-            int ks[4];
-            int m = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                ks[u] = cand ? __ffsll((unsigned long long)cand) - 1 : 0;
-                if (cand) {
-                    cand &= cand - 1;
-                    ++m;
-                }
+            const int k = 63 - __clzll((long long)cand);
+            cand &= ~(1ull << k);
+            float dk = fmaxf(dist(a, k), dist(b, k));
+            if (dim == 2) dk = fmaxf(dk, dist(c, k));
+            const uint32_t pk = dim == 1 ? tri_with(a, b, k) : tet_with(a, b, c, k);
+            if (dk <= diam) {
+                best = make_key(diam, pk);
+                break;
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (u < m) {
-                    const int k = ks[u];
-                    uint64_t key;
-                    if (dim == 1) key = make_key(fmaxf(diam, fmaxf(dist(a, k), dist(b, k))), tri_with(a, b, k));
-                    else key = make_key(fmaxf(diam, fmaxf(fmaxf(dist(a, k), dist(b, k)), dist(c, k))), tet_with(a, b, c, k));
-                    best = key < best ? key : best;
-                }
-            }
+            const uint64_t key = make_key(dk, pk);
+            best = key < best ? key : best;
         }
         return best;
     }
@@ -326,8 +318,17 @@ struct Complex {
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         bool col;
         const uint32_t f = uni(max_facet(dim, uni64(tau), col));
+#ifdef DGN_APP_FLY
+        if (!uni(col)) return kNone;
+        const int a = (f >> 16) & 255, b = (f >> 8) & 255, c = f & 255;
+        uint64_t mk;
+        if (dim == 1) mk = min_cofacet_wave(1, b, c, 0, dlow(b, c), uni64(s.adj[b]) & uni64(s.adj[c]));
+        else mk = min_cofacet_wave(2, a, b, c, tri_diam(a, b, c), uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]));
+        return mk == uni64(tau) ? f : kNone;
+#else
         const uint32_t m = sp<uint32_t>(ScratchLayout::mincof)[col_dense(dim, f)];
         return uni(m) == key_packed(tau) ? f : kNone;
+#endif
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {
@@ -348,98 +349,161 @@ struct Complex {
         return -1;
     }
 
+    // ---- the working column's V list, resident in registers: lane t holds entry t (set 0) and
+    // entry t + 64 (set 1): packed simplex, its candidate-cofacet vertex mask (adjacency
+    // intersection) and its diameter. Uniform reads are v_readlane; no LDS.
+    uint32_t vs0 = 0, vs1 = 0;
+    uint64_t vc0 = 0, vc1 = 0;
+    float vd0 = 0.f, vd1 = 0.f;
+
+    __device__ static uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+    __device__ static uint64_t rl64(uint64_t x, int l) {
+        return ((uint64_t)rl((uint32_t)(x >> 32), l) << 32) | rl((uint32_t)x, l);
+    }
+    __device__ void v_get(int i, uint32_t& sp_, uint64_t& cand, float& diam) const {
+        const int l = i & 63;
+        if (i < 64) {
+            sp_ = rl(vs0, l);
+            cand = rl64(vc0, l);
+            diam = __uint_as_float(rl(__float_as_uint(vd0), l));
+        } else {
+            sp_ = rl(vs1, l);
+            cand = rl64(vc1, l);
+            diam = __uint_as_float(rl(__float_as_uint(vd1), l));
+        }
+    }
+    __device__ void v_set(int i, uint32_t sp_, uint64_t cand, float diam) {
+        const int lane = lane_id();
+        if (i < 64) {
+            if (lane == i) { vs0 = sp_; vc0 = cand; vd0 = diam; }
+        } else if (lane == i - 64) {
+            vs1 = sp_; vc1 = cand; vd1 = diam;
+        }
+    }
+    __device__ int v_find(uint32_t x, int v) const {
+        const int lane = lane_id();
+        uint64_t bal = ballot(lane < v && vs0 == x);
+        if (bal) return __ffsll((unsigned long long)bal) - 1;
+        if (v > 64) {
+            bal = ballot(lane + 64 < v && vs1 == x);
+            if (bal) return 64 + __ffsll((unsigned long long)bal) - 1;
+        }
+        return -1;
+    }
+    // V ^= {x} (whole wave, uniform arguments); false on V-list overflow
+    __device__ bool v_toggle(int dim, uint32_t x, int& v) {
+        const int pos = v_find(x, v);
+        if (pos >= 0) {
+            if (pos != v - 1) {
+                uint32_t ls;
+                uint64_t lc;
+                float ld;
+                v_get(v - 1, ls, lc, ld);
+                v_set(pos, ls, lc, ld);
+            }
+            v = (int)uni((uint32_t)(v - 1));
+            return true;
+        }
+        if (v >= kVCap) return false;
+        uint64_t cand;
+        float diam;
+        if (dim == 1) {
+            const int a = (x >> 8) & 255, b = x & 255;
+            cand = uni64(s.adj[a]) & uni64(s.adj[b]);
+            diam = __uint_as_float(uni(__float_as_uint(dlow(a, b))));
+        } else {
+            const int a = (x >> 16) & 255, b = (x >> 8) & 255, c = x & 255;
+            cand = uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]);
+            diam = __uint_as_float(uni(__float_as_uint(tri_diam(a, b, c))));
+        }
+        v_set(v, x, cand, diam);
+        v = (int)uni((uint32_t)(v + 1));
+        return true;
+    }
+    __device__ static uint64_t vmask(int dim, uint32_t p) {
+        return dim == 1 ? ((1ull << ((p >> 8) & 255)) | (1ull << (p & 255)))
+                        : ((1ull << ((p >> 16) & 255)) | (1ull << ((p >> 8) & 255)) | (1ull << (p & 255)));
+    }
+    // OR of bit (third vertex) over V entries (except entry i) that contain both a and b
+    // (dim 2), or of bit (other vertex) over entries containing a (dim 1)
+    __device__ uint64_t facet_mask(int dim, uint64_t need, int a, int b, int i, int v, uint64_t m0, uint64_t m1) const {
+        const int lane = lane_id();
+        uint64_t out = 0;
+        uint64_t bal = ballot(lane < v && lane != i && (m0 & need) == need);
+        while (bal) {
+            const int t = __ffsll((unsigned long long)bal) - 1;
+            bal &= bal - 1;
+            const uint32_t q = rl(vs0, t);
+            const int w = dim == 1 ? (int)(((q >> 8) & 255) + (q & 255)) - a
+                                   : (int)(((q >> 16) & 255) + ((q >> 8) & 255) + (q & 255)) - a - b;
+            out |= 1ull << w;
+        }
+        if (v > 64) {
+            bal = ballot(lane + 64 < v && lane + 64 != i && (m1 & need) == need);
+            while (bal) {
+                const int t = __ffsll((unsigned long long)bal) - 1;
+                bal &= bal - 1;
+                const uint32_t q = rl(vs1, t);
+                const int w = dim == 1 ? (int)(((q >> 8) & 255) + (q & 255)) - a
+                                       : (int)(((q >> 16) & 255) + ((q >> 8) & 255) + (q & 255)) - a - b;
+                out |= 1ull << w;
+            }
+        }
+        return out;
+    }
+
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
-    // multiplicity. Cofacet tau = s u {k} is evaluated by lane k for each s in V; its other
-    // facets are found in V through the LDS bitmap, and only the packed-smallest facet of tau
-    // in V reports it (so each tau is counted once). kInf for the zero column.
+    // multiplicity. Cofacet tau = s u {k} is evaluated by lane k for each s in V. Its other
+    // facets are s with one vertex x replaced by k; they are in V iff bit k is set in the
+    // facet mask of the remaining vertices, and such a facet precedes s in index order iff
+    // k < x. Only the index-smallest facet of tau in V reports it (each tau counted once).
+    // kInf for the zero column.
     __device__ uint64_t pivot_of_V(int dim, int v_) const {
-        // Branch-free body: every lane evaluates its vertex k for every V entry (uniform terms
-        // on the scalar unit, per-lane arms selected with v_cndmask) and masks at the end.
         const int k = lane_id();
-        const int c2k = c2(k), c3k = c3(k);
+        const int c2k = c2(k);
         const int v = (int)uni((uint32_t)v_);
+        const uint64_t m0 = vmask(dim, vs0), m1 = vmask(dim, vs1);
         uint64_t best = kInf;
         for (int i = 0; i < v; ++i) {
-            const uint32_t sp_ = uni(s.vcur[i]);
+            uint32_t sp_;
+            uint64_t cand;
+            float diam;
+            v_get(i, sp_, cand, diam);
+            const bool on = (cand >> k) & 1ull;
             if (dim == 1) {
                 const int a = (sp_ >> 8) & 255, b = sp_ & 255;
-                const uint64_t cand = uni64(s.adj[a]) & uni64(s.adj[b]);
-                const int C2a = c2(a), C2b = c2(b), ds = C2a + b;
-                const float dab = __uint_as_float(uni(__float_as_uint(dlow(a, b))));
-                const bool on = (cand >> k) & 1ull;
-                const bool ga = k > a, gb = k > b;
-                const int t11 = pin(c2k + a), t12 = pin(C2a + k), t21 = pin(c2k + b), t22 = pin(C2b + k);
-                const int d1 = ga ? t11 : t12;  // {a, k}
-                const int d2 = gb ? t21 : t22;  // {b, k}
-                const bool m1 = vbit(on ? d1 : 0), m2 = vbit(on ? d2 : 0);
-                const bool odd = !(m1 ^ m2);  // 1 + m1 + m2 odd
-                const bool rep = !(m1 && d1 < ds) && !(m2 && d2 < ds);
-                // edge {a,k} / {b,k} indices are d1 / d2 (clamped for idle lanes)
-                const float dd = fmaxf(dab, fmaxf(s.Dt[on ? d1 : 0], s.Dt[on ? d2 : 0]));
+                const uint64_t Ma = facet_mask(1, 1ull << a, a, 0, i, v, m0, m1);  // {a, x} in V
+                const uint64_t Mb = facet_mask(1, 1ull << b, b, 0, i, v, m0, m1);  // {b, x} in V
+                const bool f1 = (Ma >> k) & 1ull, f2 = (Mb >> k) & 1ull;  // {a,k}, {b,k}
+                const bool odd = !(f1 ^ f2);
+                const bool rep = !(f1 && k < b) && !(f2 && k < a);
+                const int ia = k > a ? c2k + a : c2(a) + k, ib = k > b ? c2k + b : c2(b) + k;
+                const float dd = fmaxf(diam, fmaxf(s.Dt[on ? ia : 0], s.Dt[on ? ib : 0]));
                 const uint32_t p1 = pin(pack3(k, a, b)), p2 = pin(pack3(a, k, b)), p3 = pin(pack3(a, b, k));
-                const uint32_t pk = ga ? p1 : (gb ? p2 : p3);
+                const uint32_t pk = k > a ? p1 : (k > b ? p2 : p3);
                 const uint64_t key = make_key(dd, pk);
                 best = (on && odd && rep && key < best) ? key : best;
             } else {
                 const int a = (sp_ >> 16) & 255, b = (sp_ >> 8) & 255, c = sp_ & 255;
-                const uint64_t cand = uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]);
-                const int C3a = c3(a), C3b = c3(b), C2a = c2(a), C2b = c2(b), C2c = c2(c);
-                const int ds = C3a + C2b + c;
-                const float dabc = __uint_as_float(uni(__float_as_uint(tri_diam(a, b, c))));
-                const bool on = (cand >> k) & 1ull;
-                const bool ga = k > a, gb = k > b, gc = k > c;
-                // dense indices of the facets {a,b,k}, {a,c,k}, {b,c,k} (colex == index order)
-                const int t11 = pin(c3k + C2a + b), t12 = pin(C3a + c2k + b), t13 = pin(C3a + C2b + k);
-                const int t21 = pin(c3k + C2a + c), t22 = pin(C3a + c2k + c), t23 = pin(C3a + C2c + k);
-                const int t31 = pin(c3k + C2b + c), t32 = pin(C3b + c2k + c), t33 = pin(C3b + C2c + k);
-                const int d1 = ga ? t11 : (gb ? t12 : t13);
-                const int d2 = ga ? t21 : (gc ? t22 : t23);
-                const int d3 = gb ? t31 : (gc ? t32 : t33);
-                const bool m1 = vbit(on ? d1 : 0), m2 = vbit(on ? d2 : 0), m3 = vbit(on ? d3 : 0);
-                const bool odd = !(m1 ^ m2 ^ m3);
-                const bool rep = !(m1 && d1 < ds) && !(m2 && d2 < ds) && !(m3 && d3 < ds);
-                const int ea = pin(ga ? c2k + a : C2a + k), eb = pin(gb ? c2k + b : C2b + k);
-                const int ec = pin(gc ? c2k + c : C2c + k);
-                const float dd = fmaxf(dabc, fmaxf(fmaxf(s.Dt[on ? ea : 0], s.Dt[on ? eb : 0]), s.Dt[on ? ec : 0]));
+                const uint64_t Mab = facet_mask(2, (1ull << a) | (1ull << b), a, b, i, v, m0, m1);
+                const uint64_t Mac = facet_mask(2, (1ull << a) | (1ull << c), a, c, i, v, m0, m1);
+                const uint64_t Mbc = facet_mask(2, (1ull << b) | (1ull << c), b, c, i, v, m0, m1);
+                const bool f1 = (Mab >> k) & 1ull, f2 = (Mac >> k) & 1ull, f3 = (Mbc >> k) & 1ull;
+                const bool odd = !(f1 ^ f2 ^ f3);
+                const bool rep = !(f1 && k < c) && !(f2 && k < b) && !(f3 && k < a);
+                const int ia = k > a ? c2k + a : c2(a) + k, ib = k > b ? c2k + b : c2(b) + k;
+                const int ic = k > c ? c2k + c : c2(c) + k;
+                const float dd =
+                    fmaxf(diam, fmaxf(fmaxf(s.Dt[on ? ia : 0], s.Dt[on ? ib : 0]), s.Dt[on ? ic : 0]));
                 const uint32_t pabc = pack3(a, b, c);
                 const uint32_t p1 = pin(((uint32_t)k << 24) | pabc), p2 = pin(pack4(a, k, b, c));
                 const uint32_t p3 = pin(pack4(a, b, k, c)), p4 = pin((pabc << 8) | (uint32_t)k);
-                const uint32_t pk = ga ? p1 : (gb ? p2 : (gc ? p3 : p4));
+                const uint32_t pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
                 const uint64_t key = make_key(dd, pk);
                 best = (on && odd && rep && key < best) ? key : best;
             }
         }
         return wave_min_u64(best);
-    }
-
-    // V ^= {x}: toggle one simplex in the current V list (whole wave, uniform arguments)
-    __device__ bool v_toggle(int dim, uint32_t x, int& v) {
-        const int lane = lane_id();
-        const int idx = col_dense(dim, x);
-        if (uni(vbit(idx))) {
-            int pos = -1;
-            v = (int)uni((uint32_t)v);
-            for (int base = 0; base < v && pos < 0; base += kWave) {
-                const uint64_t bal = ballot(base + lane < v && s.vcur[base + lane] == x);
-                if (bal) pos = base + __ffsll((unsigned long long)bal) - 1;
-            }
-            const uint32_t last = uni(s.vcur[v - 1]);
-            lds_sync();
-            if (lane == 0) {
-                s.vcur[pos] = last;
-                atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
-            }
-            v = (int)uni((uint32_t)(v - 1));
-        } else {
-            if (v >= kVCap) return false;
-            if (lane == 0) {
-                s.vcur[v] = x;
-                atomicOr(&s.vbits[idx >> 5], 1u << (idx & 31));
-            }
-            v = (int)uni((uint32_t)(v + 1));
-        }
-        lds_sync();
-        return true;
     }
 
     // Walk the non-apparent columns in Ripser's order (whole wave). na_* arrays hold each
@@ -520,15 +584,7 @@ struct Complex {
                     if (owner < 0 && app == kNone) break;  // tau is this column's pivot
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
-                if (tau == kInf) {
-                    // clear the membership bits of the (zero) column's V
-                    for (int t = lane; t < v; t += kWave) {
-                        const int idx = col_dense(dim, s.vcur[t]);
-                        atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
-                    }
-                    lds_sync();
-                    continue;
-                }
+                if (tau == kInf) continue;  // zero column
             }
             // ---- tau is the pivot of this column ----
             const float death = key_diam(tau);
@@ -551,11 +607,9 @@ struct Complex {
             } else {
                 if (vused + v > kVStoreCap || v > 511) { err |= kErrR; return; }
                 for (int t = lane; t < v; t += kWave) {
-                    const uint32_t x = s.vcur[t];
+                    const uint32_t x = t < kWave ? vs0 : vs1;
                     if (vused + t < kVStoreLds) s.vstore[vused + t] = x;
                     else gvstore[vused + t] = x;
-                    const int idx = col_dense(dim, x);
-                    atomicAnd(&s.vbits[idx >> 5], ~(1u << (idx & 31)));
                 }
                 meta = ((uint32_t)vused << 9) | (uint32_t)v;
                 vused = (int)uni((uint32_t)(vused + v));
@@ -719,10 +773,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 s.adj[lane] = lane < n ? m : 0ull;
                 s.tree[lane] = 0ull;
             }
-            for (int i = lane; i < (int)(sizeof(s.cleared) / 4); i += kWave) {
-                s.cleared[i] = 0u;
-                s.vbits[i] = 0u;
-            }
+            for (int i = lane; i < (int)(sizeof(s.cleared) / 4); i += kWave) s.cleared[i] = 0u;
             lds_sync();
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
