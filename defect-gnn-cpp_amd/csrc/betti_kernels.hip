@@ -574,6 +574,11 @@ struct Complex {
                     if (!ok) { err |= kErrWorkCol; return; }
                     ++n_adds;
                     DGN_SUB(20);
+#ifdef DGN_PHASE_TIMING
+                    ph[14] += (uint64_t)v;
+                    ph[15] += (uint64_t)v * (uint64_t)v;
+                    ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
+#endif
                     tau = v > 0 ? pivot_of_V(dim, v) : kInf;
                     DGN_SUB(21);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
@@ -1046,7 +1051,8 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     }
 #ifdef DGN_PHASE_TIMING
     if (lane == 0 && bl.phase_cycles)
-        for (int k = 0; k < 24; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
+        for (int k = 0; k < 23; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
+    if (lane == 0 && bl.phase_cycles) atomicMax(&bl.phase_cycles[23], (unsigned long long)ph[23]);
 #endif
 }
 

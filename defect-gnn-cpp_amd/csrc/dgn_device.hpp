@@ -23,7 +23,7 @@ struct StructMeta {
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // number of set bits of m strictly below this lane
 __device__ __forceinline__ int mask_prefix(uint64_t m) {

@@ -21,9 +21,13 @@ ctx = dgn.Context(0)
 batch = dgn.synth_batch(kind, m, B)
 A = batch["positions"].shape[0]
 ctx.host_betti(batch, rc)  # warm-up
+ctx.reset_timing()
+ctx.enable_timing(True)
 t0 = time.perf_counter()
 f, c = ctx.host_betti(batch, rc)
 dt = time.perf_counter() - t0
+kt = ctx.kernel_times()
+ctx.enable_timing(False)
 ph = (C.c_ulonglong * 24)()
 dgn.lib().dgn_diag_phase_cycles(ctx.h, ph)
 ph = list(ph)
@@ -32,9 +36,12 @@ names = ["load+gram", "adj+prim+edges", "dim1 apparent", "dim1 serial", "dim2 ap
 sub = ["serial:sort", "serial:col-start", "serial:find_pivot", "serial:apparent_owner", "serial:toggles", "serial:pivot_of_V", "serial:finalize"]
 tot = sum(ph[:8]) + sum(ph[16:23])
 out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round(dt, 4),
+       "betti_vr_ms": round(kt.get("betti_vr", {}).get("total_ms", 0.0), 3),
        "cycles_per_complex": round(tot / A), "phase_cycles_per_complex": {n: round(ph[i] / A) for i, n in enumerate(names)},
        "phase_share": {n: round(ph[i] / tot, 4) for i, n in enumerate(names)},
        "na1_per_complex": ph[8] / A, "na2_per_complex": ph[9] / A, "adds1": ph[10] / A, "adds2": ph[11] / A,
        "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13],
+       "pivot_V_entries_per_complex": ph[14] / A, "pivot_V_sq_per_complex": ph[15] / A,
+       "max_V": ph[23],
        "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
 print(json.dumps(out, indent=1))
