@@ -34,10 +34,8 @@ namespace dgn {
 
 constexpr int kVCap = 128;        // simplices in one column's V list (registers: 2 per lane)
 constexpr int kVStoreLds = 128;   // stored V-list entries kept in LDS (rest in scratch)
-constexpr int kNALds = 64;        // sorted non-apparent column records kept in LDS
 constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
 constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
-constexpr int kPivLds = 64;       // serially resolved pivots kept in LDS (rest in scratch)
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
 constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
 constexpr int kChunk = 4;         // complexes per dequeue
@@ -84,14 +82,8 @@ struct BettiSmem {
             double X[NP][3];
             double sq[NP];
         } cloud;
-        struct {
-            uint64_t key[kNALds];
-            uint64_t tau[kNALds];
-        } na;
     } u;
     uint32_t vstore[kVStoreLds];
-    uint64_t piv[kPivLds];
-    uint32_t vmeta[kPivLds];
     float d0[NP];
 };
 
@@ -335,23 +327,48 @@ struct Complex {
         return dim == 1 ? ekey((cp >> 8) & 255, cp & 255) : tkey((cp >> 16) & 255, (cp >> 8) & 255, cp & 255);
     }
 
-    // serially resolved pivot table: find tau (whole wave)
+    // ---- serially resolved pivot table: entries 0..127 in registers (lane t holds entries t
+    // and t + 64: pivot key and V-list descriptor), the rest in scratch
+    uint64_t pk0 = 0, pk1 = 0;
+    uint32_t pm0 = 0, pm1 = 0;
+
     __device__ int find_pivot(int npiv, uint64_t tau) const {
         const int lane = lane_id();
+        uint64_t bal = ballot(lane < npiv && pk0 == tau);
+        if (bal) return __ffsll((unsigned long long)bal) - 1;
+        if (npiv > kWave) {
+            bal = ballot(lane + kWave < npiv && pk1 == tau);
+            if (bal) return kWave + __ffsll((unsigned long long)bal) - 1;
+        }
         const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
-        for (int base = 0; base < npiv; base += kWave) {
+        for (int base = 2 * kWave; base < npiv; base += kWave) {
             const int i = base + lane;
-            bool hit = false;
-            if (i < npiv) hit = (i < kPivLds ? s.piv[i] : sp_piv[i]) == tau;
-            const uint64_t bal = ballot(hit);
+            bal = ballot(i < npiv && sp_piv[i] == tau);
             if (bal) return base + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
     }
+    __device__ uint32_t piv_meta(int i) const {
+        if (i < kWave) return rl(pm0, i);
+        if (i < 2 * kWave) return rl(pm1, i - kWave);
+        return uni(sp<uint32_t>(ScratchLayout::vmeta)[i]);
+    }
+    __device__ void piv_push(int i, uint64_t tau, uint32_t meta) {
+        const int lane = lane_id();
+        if (i < kWave) {
+            if (lane == i) { pk0 = tau; pm0 = meta; }
+        } else if (i < 2 * kWave) {
+            if (lane == i - kWave) { pk1 = tau; pm1 = meta; }
+        } else if (lane == 0) {
+            sp<uint64_t>(ScratchLayout::piv)[i] = tau;
+            sp<uint32_t>(ScratchLayout::vmeta)[i] = meta;
+        }
+    }
 
     // ---- the working column's V list, resident in registers: lane t holds entry t (set 0) and
-    // entry t + 64 (set 1): packed simplex, its candidate-cofacet vertex mask (adjacency
-    // intersection) and its diameter. Uniform reads are v_readlane; no LDS.
+    // entry t + 64 (set 1). Toggles only move packed simplices; pivot_of_V refreshes each
+    // entry's candidate-cofacet mask and diameter lane-parallel (one LDS round trip for all
+    // entries) and reads them back uniformly with v_readlane.
     uint32_t vs0 = 0, vs1 = 0;
     uint64_t vc0 = 0, vc1 = 0;
     float vd0 = 0.f, vd1 = 0.f;
@@ -372,12 +389,12 @@ struct Complex {
             diam = __uint_as_float(rl(__float_as_uint(vd1), l));
         }
     }
-    __device__ void v_set(int i, uint32_t sp_, uint64_t cand, float diam) {
+    __device__ void v_set(int i, uint32_t sp_) {
         const int lane = lane_id();
         if (i < 64) {
-            if (lane == i) { vs0 = sp_; vc0 = cand; vd0 = diam; }
+            if (lane == i) vs0 = sp_;
         } else if (lane == i - 64) {
-            vs1 = sp_; vc1 = cand; vd1 = diam;
+            vs1 = sp_;
         }
     }
     __device__ int v_find(uint32_t x, int v) const {
@@ -391,34 +408,28 @@ struct Complex {
         return -1;
     }
     // V ^= {x} (whole wave, uniform arguments); false on V-list overflow
-    __device__ bool v_toggle(int dim, uint32_t x, int& v) {
+    __device__ bool v_toggle(int, uint32_t x, int& v) {
         const int pos = v_find(x, v);
         if (pos >= 0) {
-            if (pos != v - 1) {
-                uint32_t ls;
-                uint64_t lc;
-                float ld;
-                v_get(v - 1, ls, lc, ld);
-                v_set(pos, ls, lc, ld);
-            }
+            if (pos != v - 1) v_set(pos, v - 1 < 64 ? rl(vs0, v - 1) : rl(vs1, v - 65));
             v = (int)uni((uint32_t)(v - 1));
             return true;
         }
         if (v >= kVCap) return false;
-        uint64_t cand;
-        float diam;
-        if (dim == 1) {
-            const int a = (x >> 8) & 255, b = x & 255;
-            cand = uni64(s.adj[a]) & uni64(s.adj[b]);
-            diam = __uint_as_float(uni(__float_as_uint(dlow(a, b))));
-        } else {
-            const int a = (x >> 16) & 255, b = (x >> 8) & 255, c = x & 255;
-            cand = uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]);
-            diam = __uint_as_float(uni(__float_as_uint(tri_diam(a, b, c))));
-        }
-        v_set(v, x, cand, diam);
+        v_set(v, x);
         v = (int)uni((uint32_t)(v + 1));
         return true;
+    }
+    __device__ void simplex_info(int dim, uint32_t x, uint64_t& cand, float& diam) const {
+        if (dim == 1) {
+            const int a = (x >> 8) & 255, b = x & 255;
+            cand = s.adj[a] & s.adj[b];
+            diam = dlow(a, b);
+        } else {
+            const int a = (x >> 16) & 255, b = (x >> 8) & 255, c = x & 255;
+            cand = s.adj[a] & s.adj[b] & s.adj[c];
+            diam = tri_diam(a, b, c);
+        }
     }
     __device__ static uint64_t vmask(int dim, uint32_t p) {
         return dim == 1 ? ((1ull << ((p >> 8) & 255)) | (1ull << (p & 255)))
@@ -458,11 +469,14 @@ struct Complex {
     // facet mask of the remaining vertices, and such a facet precedes s in index order iff
     // k < x. Only the index-smallest facet of tau in V reports it (each tau counted once).
     // kInf for the zero column.
-    __device__ uint64_t pivot_of_V(int dim, int v_) const {
+    __device__ uint64_t pivot_of_V(int dim, int v_) {
         const int k = lane_id();
         const int c2k = c2(k);
         const int v = (int)uni((uint32_t)v_);
         const uint64_t m0 = vmask(dim, vs0), m1 = vmask(dim, vs1);
+        // refresh the entries' cofacet masks and diameters (lane-parallel)
+        if (k < v) simplex_info(dim, vs0, vc0, vd0);
+        if (v > 64 && k + 64 < v) simplex_info(dim, vs1, vc1, vd1);
         uint64_t best = kInf;
         for (int i = 0; i < v; ++i) {
             uint32_t sp_;
@@ -506,19 +520,52 @@ struct Complex {
         return wave_min_u64(best);
     }
 
-    // Walk the non-apparent columns in Ripser's order (whole wave). na_* arrays hold each
-    // column's key and its unreduced pivot.
+    // per-lane apparent owner of pivot tau (kNone if none): its F-max facet f, if tau is f's
+    // F-minimal cofacet (recorded for every column by the lane-parallel pass)
+    __device__ uint32_t apparent_owner_lane(int dim, uint64_t tau) const {
+        bool col;
+        const uint32_t f = max_facet(dim, tau, col);
+        const uint32_t m = sp<uint32_t>(ScratchLayout::mincof)[col_dense(dim, f)];
+        return m == key_packed(tau) ? f : kNone;
+    }
+
+    // Walk the non-apparent columns in Ripser's order (whole wave). na_* (scratch) hold each
+    // column's key and its unreduced pivot. Up to 128 records live in registers (lane t:
+    // records t and t + 64) with their rank in column order and the apparent owner of their
+    // initial pivot, all computed lane-parallel; larger sets are rank-sorted into scratch.
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
         if (nna > kNACap) { err |= kErrNA; return; }
-        // ---- sort by column key DESCENDING (rank sort). Sorted (key, pivot) records go to LDS
-        // when they fit (they are read back one per column, in order), else to scratch.
-        const bool in_lds = nna <= kNALds;
-        uint64_t* sk = in_lds ? s.u.na.key : sp<uint64_t>(ScratchLayout::sna_key);
-        uint64_t* st = in_lds ? s.u.na.tau : sp<uint64_t>(ScratchLayout::sna_tau);
-        {
-            const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
-            const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
+        const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
+        const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
+        const bool regs = nna <= 2 * kWave;
+        uint64_t rk0 = 0, rk1 = 0, rt0 = 0, rt1 = 0;
+        int rr0 = -1, rr1 = -1;
+        uint32_t ra0 = kNone, ra1 = kNone;
+        uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
+        uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
+        if (regs) {
+            if (lane < nna) { rk0 = gk[lane]; rt0 = gt[lane]; }
+            if (lane + kWave < nna) { rk1 = gk[lane + kWave]; rt1 = gt[lane + kWave]; }
+            // rank by column key DESCENDING (Ripser processes columns in decreasing F-order)
+            int r0 = 0, r1 = 0;
+            const int n0 = nna < kWave ? nna : kWave;
+            for (int u = 0; u < n0; ++u) {
+                const uint64_t ku = rl64(rk0, u);
+                r0 += ku > rk0;
+                r1 += ku > rk1;
+            }
+            for (int u = kWave; u < nna; ++u) {
+                const uint64_t ku = rl64(rk1, u - kWave);
+                r0 += ku > rk0;
+                r1 += ku > rk1;
+            }
+            rr0 = lane < nna ? r0 : -1;
+            rr1 = lane + kWave < nna ? r1 : -1;
+            // apparent owners of the initial pivots (global loads overlap across lanes)
+            if (lane < nna) ra0 = apparent_owner_lane(dim, rt0);
+            if (lane + kWave < nna) ra1 = apparent_owner_lane(dim, rt1);
+        } else {
             for (int i = lane; i < nna; i += kWave) {
                 const uint64_t v = gk[i];
                 int rank = 0;
@@ -529,24 +576,37 @@ struct Complex {
             __syncthreads();
         }
         DGN_SUB(16);
-        uint32_t* gvmeta = sp<uint32_t>(ScratchLayout::vmeta);
-        uint64_t* gpiv = sp<uint64_t>(ScratchLayout::piv);
         uint32_t* gvstore = sp<uint32_t>(ScratchLayout::vstore);
         int npiv = 0, vused = 0;
-        uint64_t nk = nna > 0 ? uni64(sk[0]) : 0, nt = nna > 0 ? uni64(st[0]) : 0;
         for (int ci = 0; ci < nna; ++ci) {
-            const uint64_t colkey = nk;
-            uint64_t tau = nt;
-            if (ci + 1 < nna) {  // prefetch the next column's record
-                nk = uni64(sk[ci + 1]);
-                nt = uni64(st[ci + 1]);
+            uint64_t colkey, tau;
+            uint32_t app0 = kNone;
+            bool have_app = false;
+            if (regs) {
+                uint64_t bal = ballot(rr0 == ci);
+                if (bal) {
+                    const int l = __ffsll((unsigned long long)bal) - 1;
+                    colkey = rl64(rk0, l);
+                    tau = rl64(rt0, l);
+                    app0 = rl(ra0, l);
+                } else {
+                    bal = ballot(rr1 == ci);
+                    const int l = __ffsll((unsigned long long)bal) - 1;
+                    colkey = rl64(rk1, l);
+                    tau = rl64(rt1, l);
+                    app0 = rl(ra1, l);
+                }
+                have_app = true;
+            } else {
+                colkey = uni64(sk[ci]);
+                tau = uni64(st[ci]);
             }
             const uint32_t cp = key_packed(colkey);
             const float birth = key_diam(colkey);
             DGN_SUB(17);
             int owner = find_pivot(npiv, tau);
             DGN_SUB(18);
-            uint32_t app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+            uint32_t app = owner >= 0 ? kNone : (have_app ? app0 : apparent_owner_wave(dim, tau));
             DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
             if (owner >= 0 || app != kNone) {
@@ -560,7 +620,7 @@ struct Complex {
                         if (!(column_key(dim, app) > colkey)) { err |= kErrOrder; return; }
                         ok = v_toggle(dim, app, v);
                     } else {
-                        const uint32_t m = uni(owner < kPivLds ? s.vmeta[owner] : gvmeta[owner]);
+                        const uint32_t m = piv_meta(owner);
                         if (m & kLazyBit) {
                             ok = v_toggle(dim, m & ~kLazyBit, v);
                         } else {
@@ -619,15 +679,7 @@ struct Complex {
                 meta = ((uint32_t)vused << 9) | (uint32_t)v;
                 vused = (int)uni((uint32_t)(vused + v));
             }
-            if (lane == 0) {
-                if (npiv < kPivLds) {
-                    s.piv[npiv] = tau;
-                    s.vmeta[npiv] = meta;
-                } else {
-                    gpiv[npiv] = tau;
-                    gvmeta[npiv] = meta;
-                }
-            }
+            piv_push(npiv, tau, meta);
             npiv = (int)uni((uint32_t)(npiv + 1));
             lds_sync();
             DGN_SUB(22);
