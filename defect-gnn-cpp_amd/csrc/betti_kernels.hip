@@ -366,28 +366,15 @@ struct Complex {
     }
 
     // ---- the working column's V list, resident in registers: lane t holds entry t (set 0) and
-    // entry t + 64 (set 1). Toggles only move packed simplices; pivot_of_V refreshes each
-    // entry's candidate-cofacet mask and diameter lane-parallel (one LDS round trip for all
-    // entries) and reads them back uniformly with v_readlane.
+    // entry t + 64 (set 1) with its diameter. Toggles only move packed simplices; pivot_of_V
+    // refreshes the diameters lane-parallel and reads entries back uniformly with v_readlane.
     uint32_t vs0 = 0, vs1 = 0;
-    uint64_t vc0 = 0, vc1 = 0;
     float vd0 = 0.f, vd1 = 0.f;
+    uint64_t myadj = 0;  // lane k: adjacency row of vertex k (cofacet candidates test bits of it)
 
     __device__ static uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
     __device__ static uint64_t rl64(uint64_t x, int l) {
         return ((uint64_t)rl((uint32_t)(x >> 32), l) << 32) | rl((uint32_t)x, l);
-    }
-    __device__ void v_get(int i, uint32_t& sp_, uint64_t& cand, float& diam) const {
-        const int l = i & 63;
-        if (i < 64) {
-            sp_ = rl(vs0, l);
-            cand = rl64(vc0, l);
-            diam = __uint_as_float(rl(__float_as_uint(vd0), l));
-        } else {
-            sp_ = rl(vs1, l);
-            cand = rl64(vc1, l);
-            diam = __uint_as_float(rl(__float_as_uint(vd1), l));
-        }
     }
     __device__ void v_set(int i, uint32_t sp_) {
         const int lane = lane_id();
@@ -420,104 +407,89 @@ struct Complex {
         v = (int)uni((uint32_t)(v + 1));
         return true;
     }
-    __device__ void simplex_info(int dim, uint32_t x, uint64_t& cand, float& diam) const {
-        if (dim == 1) {
-            const int a = (x >> 8) & 255, b = x & 255;
-            cand = s.adj[a] & s.adj[b];
-            diam = dlow(a, b);
-        } else {
-            const int a = (x >> 16) & 255, b = (x >> 8) & 255, c = x & 255;
-            cand = s.adj[a] & s.adj[b] & s.adj[c];
-            diam = tri_diam(a, b, c);
-        }
-    }
-    __device__ static uint64_t vmask(int dim, uint32_t p) {
-        return dim == 1 ? ((1ull << ((p >> 8) & 255)) | (1ull << (p & 255)))
-                        : ((1ull << ((p >> 16) & 255)) | (1ull << ((p >> 8) & 255)) | (1ull << (p & 255)));
-    }
-    // OR of bit (third vertex) over V entries (except entry i) that contain both a and b
-    // (dim 2), or of bit (other vertex) over entries containing a (dim 1)
-    __device__ uint64_t facet_mask(int dim, uint64_t need, int a, int b, int i, int v, uint64_t m0, uint64_t m1) const {
-        const int lane = lane_id();
-        uint64_t out = 0;
-        uint64_t bal = ballot(lane < v && lane != i && (m0 & need) == need);
-        while (bal) {
-            const int t = __ffsll((unsigned long long)bal) - 1;
-            bal &= bal - 1;
-            const uint32_t q = rl(vs0, t);
-            const int w = dim == 1 ? (int)(((q >> 8) & 255) + (q & 255)) - a
-                                   : (int)(((q >> 16) & 255) + ((q >> 8) & 255) + (q & 255)) - a - b;
-            out |= 1ull << w;
-        }
-        if (v > 64) {
-            bal = ballot(lane + 64 < v && lane + 64 != i && (m1 & need) == need);
-            while (bal) {
-                const int t = __ffsll((unsigned long long)bal) - 1;
-                bal &= bal - 1;
-                const uint32_t q = rl(vs1, t);
-                const int w = dim == 1 ? (int)(((q >> 8) & 255) + (q & 255)) - a
-                                       : (int)(((q >> 16) & 255) + ((q >> 8) & 255) + (q & 255)) - a - b;
-                out |= 1ull << w;
-            }
-        }
-        return out;
+    __device__ float simplex_diam(int dim, uint32_t x) const {
+        return dim == 1 ? dlow((x >> 8) & 255, x & 255) : tri_diam((x >> 16) & 255, (x >> 8) & 255, x & 255);
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
-    // multiplicity. Cofacet tau = s u {k} is evaluated by lane k for each s in V. Its other
-    // facets are s with one vertex x replaced by k; they are in V iff bit k is set in the
-    // facet mask of the remaining vertices, and such a facet precedes s in index order iff
-    // k < x. Only the index-smallest facet of tau in V reports it (each tau counted once).
+    // multiplicity, restricted to keys above `floor` (the column's previous pivot: adding the
+    // owner column cancels it and every other entry of both columns is larger). Lane k
+    // evaluates the cofacet s u {k} of every s in V; one cofacet tau arises once per facet of
+    // tau in V, always in a different lane (k = tau \ s), so the multiplicity of the wave
+    // minimum is the popcount of a ballot. Even multiplicity: raise the floor and repeat.
     // kInf for the zero column.
-    __device__ uint64_t pivot_of_V(int dim, int v_) {
-        const int k = lane_id();
-        const int c2k = c2(k);
-        const int v = (int)uni((uint32_t)v_);
-        const uint64_t m0 = vmask(dim, vs0), m1 = vmask(dim, vs1);
-        // refresh the entries' cofacet masks and diameters (lane-parallel)
-        if (k < v) simplex_info(dim, vs0, vc0, vd0);
-        if (v > 64 && k + 64 < v) simplex_info(dim, vs1, vc1, vd1);
-        uint64_t best = kInf;
-        for (int i = 0; i < v; ++i) {
-            uint32_t sp_;
-            uint64_t cand;
-            float diam;
-            v_get(i, sp_, cand, diam);
-            const bool on = (cand >> k) & 1ull;
-            if (dim == 1) {
-                const int a = (sp_ >> 8) & 255, b = sp_ & 255;
-                const uint64_t Ma = facet_mask(1, 1ull << a, a, 0, i, v, m0, m1);  // {a, x} in V
-                const uint64_t Mb = facet_mask(1, 1ull << b, b, 0, i, v, m0, m1);  // {b, x} in V
-                const bool f1 = (Ma >> k) & 1ull, f2 = (Mb >> k) & 1ull;  // {a,k}, {b,k}
-                const bool odd = !(f1 ^ f2);
-                const bool rep = !(f1 && k < b) && !(f2 && k < a);
-                const int ia = k > a ? c2k + a : c2(a) + k, ib = k > b ? c2k + b : c2(b) + k;
-                const float dd = fmaxf(diam, fmaxf(s.Dt[on ? ia : 0], s.Dt[on ? ib : 0]));
-                const uint32_t p1 = pin(pack3(k, a, b)), p2 = pin(pack3(a, k, b)), p3 = pin(pack3(a, b, k));
-                const uint32_t pk = k > a ? p1 : (k > b ? p2 : p3);
-                const uint64_t key = make_key(dd, pk);
-                best = (on && odd && rep && key < best) ? key : best;
-            } else {
-                const int a = (sp_ >> 16) & 255, b = (sp_ >> 8) & 255, c = sp_ & 255;
-                const uint64_t Mab = facet_mask(2, (1ull << a) | (1ull << b), a, b, i, v, m0, m1);
-                const uint64_t Mac = facet_mask(2, (1ull << a) | (1ull << c), a, c, i, v, m0, m1);
-                const uint64_t Mbc = facet_mask(2, (1ull << b) | (1ull << c), b, c, i, v, m0, m1);
-                const bool f1 = (Mab >> k) & 1ull, f2 = (Mac >> k) & 1ull, f3 = (Mbc >> k) & 1ull;
-                const bool odd = !(f1 ^ f2 ^ f3);
-                const bool rep = !(f1 && k < c) && !(f2 && k < b) && !(f3 && k < a);
-                const int ia = k > a ? c2k + a : c2(a) + k, ib = k > b ? c2k + b : c2(b) + k;
-                const int ic = k > c ? c2k + c : c2(c) + k;
-                const float dd =
-                    fmaxf(diam, fmaxf(fmaxf(s.Dt[on ? ia : 0], s.Dt[on ? ib : 0]), s.Dt[on ? ic : 0]));
-                const uint32_t pabc = pack3(a, b, c);
-                const uint32_t p1 = pin(((uint32_t)k << 24) | pabc), p2 = pin(pack4(a, k, b, c));
-                const uint32_t p3 = pin(pack4(a, b, k, c)), p4 = pin((pabc << 8) | (uint32_t)k);
-                const uint32_t pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
-                const uint64_t key = make_key(dd, pk);
-                best = (on && odd && rep && key < best) ? key : best;
-            }
+    // key of the cofacet s u {k} for lane k (kInf if k is not a common neighbour of s or the
+    // key is not above floor). Branch-free: the lower-triangle index of (k, x) is
+    // c2(max) + min, so no lane-divergent selects between scalar and vector arms.
+    __device__ uint64_t cofacet_key_above(int dim, int k, uint32_t sp_, float diam, uint64_t floor) const {
+        const int a = dim == 1 ? (int)((sp_ >> 8) & 255) : (int)((sp_ >> 16) & 255);
+        const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
+        const int c = (int)(sp_ & 255);
+        const bool on = dim == 1 ? ((myadj >> a) & (myadj >> b) & 1ull) != 0
+                                 : ((myadj >> a) & (myadj >> b) & (myadj >> c) & 1ull) != 0;
+        // every arm is materialized (pin) so the selects stay v_cndmask, never exec branches
+        const int msk = -(int)on;
+        const int ha = max(k, a), la = min(k, a), hb = max(k, b), lb = min(k, b);
+        const int ia = pin(((ha * (ha - 1)) >> 1) + la) & msk;
+        const int ib = pin(((hb * (hb - 1)) >> 1) + lb) & msk;
+        float dd = fmaxf(diam, fmaxf(s.Dt[ia], s.Dt[ib]));
+        uint32_t pk;
+        const uint32_t uk = (uint32_t)k;
+        if (dim == 1) {
+            // insert k into (a > b): k > a -> (k,a,b); a > k > b -> (a,k,b); else (a,b,k)
+            const uint32_t ab = sp_ & 0xFFFFu;
+            const uint32_t p1 = pin((uk << 16) | ab);
+            const uint32_t p2 = pin(((uint32_t)a << 16) | (uk << 8) | (uint32_t)b);
+            const uint32_t p3 = pin((ab << 8) | uk);
+            pk = k > a ? p1 : (k > b ? p2 : p3);
+        } else {
+            const int hc = max(k, c), lc = min(k, c);
+            const int ic = pin(((hc * (hc - 1)) >> 1) + lc) & msk;
+            dd = fmaxf(dd, s.Dt[ic]);
+            const uint32_t abc = sp_ & 0xFFFFFFu;
+            const uint32_t p1 = pin((uk << 24) | abc);
+            const uint32_t p2 = pin(((uint32_t)a << 24) | (uk << 16) | (abc & 0xFFFFu));
+            const uint32_t p3 = pin(((abc >> 8) << 16) | (uk << 8) | (uint32_t)c);
+            const uint32_t p4 = pin((abc << 8) | uk);
+            pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
         }
-        return wave_min_u64(best);
+        const uint64_t key = make_key(dd, pk);
+        return (on && key > floor) ? key : kInf;
+    }
+
+    // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
+    // multiplicity, restricted to keys above `floor` (the column's previous pivot: adding the
+    // owner column cancels it and every other entry of both columns is larger). Lane k
+    // evaluates the cofacet s u {k} of every s in V; one cofacet tau arises once per facet of
+    // tau in V, always in a different lane (k = tau \ s), so the multiplicity of the wave
+    // minimum is the popcount of a ballot. Even multiplicity: raise the floor and repeat.
+    // kInf for the zero column.
+    __device__ uint64_t pivot_of_V(int dim, int v_, uint64_t floor) {
+        const int k = lane_id();
+        const int v = (int)uni((uint32_t)v_);
+        const int v0 = v < 64 ? v : 64;
+        if (k < v) vd0 = simplex_diam(dim, vs0);
+        if (v > 64 && k + 64 < v) vd1 = simplex_diam(dim, vs1);
+        for (;;) {
+            uint64_t lmin = kInf;
+            for (int i = 0; i < v0; ++i) {
+                const uint64_t key = cofacet_key_above(dim, k, rl(vs0, i), __uint_as_float(rl(__float_as_uint(vd0), i)), floor);
+                lmin = key < lmin ? key : lmin;
+            }
+            for (int i = 64; i < v; ++i) {
+                const uint64_t key =
+                    cofacet_key_above(dim, k, rl(vs1, i - 64), __uint_as_float(rl(__float_as_uint(vd1), i - 64)), floor);
+                lmin = key < lmin ? key : lmin;
+            }
+            const uint64_t m = wave_min_u64(lmin);
+#ifdef DGN_PHASE_TIMING
+            ph[24] += 1;
+            ph[25] += (uint64_t)v;
+#endif
+            if (m == kInf) return kInf;
+            if (__popcll(ballot(lmin == m)) & 1) return m;
+            floor = m;
+        }
     }
 
     // per-lane apparent owner of pivot tau (kNone if none): its F-max facet f, if tau is f's
@@ -536,6 +508,7 @@ struct Complex {
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
         if (nna > kNACap) { err |= kErrNA; return; }
+        myadj = lane < n ? s.adj[lane] : 0ull;
         const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
         const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
         const bool regs = nna <= 2 * kWave;
@@ -639,7 +612,7 @@ struct Complex {
                     ph[15] += (uint64_t)v * (uint64_t)v;
                     ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
 #endif
-                    tau = v > 0 ? pivot_of_V(dim, v) : kInf;
+                    tau = v > 0 ? pivot_of_V(dim, v, tau) : kInf;
                     DGN_SUB(21);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
                     owner = find_pivot(npiv, tau);
@@ -705,7 +678,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
     __shared__ int64_t chunk_s;
 #ifdef DGN_PHASE_TIMING
-    uint64_t ph[24] = {0};
+    uint64_t ph[32] = {0};
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();
@@ -1103,7 +1076,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     }
 #ifdef DGN_PHASE_TIMING
     if (lane == 0 && bl.phase_cycles)
-        for (int k = 0; k < 23; ++k) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
+        for (int k = 0; k < 32; ++k) if (k != 23) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
     if (lane == 0 && bl.phase_cycles) atomicMax(&bl.phase_cycles[23], (unsigned long long)ph[23]);
 #endif
 }

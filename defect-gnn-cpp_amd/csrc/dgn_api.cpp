@@ -93,7 +93,7 @@ struct dgn_ctx {
     DevBuf h_lat, h_pos, h_spec, h_off;
 #ifdef DGN_PHASE_TIMING
     DevBuf phase;
-    unsigned long long phase_host[24] = {0};
+    unsigned long long phase_host[32] = {0};
 #endif
     // timing
     bool timing = false;
@@ -346,8 +346,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.pairs_out = pairs_out;
     bl.pair_cap = pair_cap;
 #ifdef DGN_PHASE_TIMING
-    HIP_TRY(c, c->phase.ensure(24 * sizeof(unsigned long long)));
-    HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 24 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(c, c->phase.ensure(32 * sizeof(unsigned long long)));
+    HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
     bl.phase_cycles = c->phase.as<unsigned long long>();
 #endif
     {

@@ -87,7 +87,7 @@ struct BettiLaunch {
     // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
     float* pairs_out;
     int32_t pair_cap;
-    unsigned long long* phase_cycles;  // [24] diagnostics build only (DGN_PHASE_TIMING)
+    unsigned long long* phase_cycles;  // [32] diagnostics build only (DGN_PHASE_TIMING)
     // set by launch_betti per launch
     const int32_t* work_list; // null = all complexes 0..num_atoms-1
     uint32_t* queue;          // work counter of this launch
