@@ -33,7 +33,6 @@
 namespace dgn {
 
 constexpr int kVCap = 128;        // simplices in one column's V list (registers: 2 per lane)
-constexpr int kVStoreLds = 128;   // stored V-list entries kept in LDS (rest in scratch)
 constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
 constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
@@ -43,6 +42,7 @@ constexpr int kChunk = 4;         // complexes per dequeue
 constexpr uint64_t kInf = ~0ull;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLazyBit = 0x80000000u;  // vmeta: V = {column simplex} (packed in the low bits)
+constexpr uint32_t kCleared = 0xC0000000u;  // mincof triangle mark (no packed tetrahedron has bit 31)
 
 // error bits (mirrored in dgn_api.cpp)
 constexpr uint32_t kErrTooManyPoints = 1u << 0;
@@ -65,26 +65,22 @@ struct ScratchLayout {
     static constexpr int64_t p2 = p1 + 8 * kPairCap;                 // float2 [kPairCap]
     static constexpr int64_t vstore = p2 + 8 * kPairCap;             // uint32 [kVStoreCap]
     // F-minimal cofacet (packed) of every edge / triangle of the complex, indexed by its dense
-    // combinatorial index; kNone for simplices that are not columns or have no cofacet
-    static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint32 [C(64,3)]
-    static constexpr int64_t total = mincof + 4 * (64 * 63 * 62 / 6);
+    // combinatorial index; kNone for simplices that are not columns or have no cofacet. Before
+    // the dim-2 pass a triangle entry may hold kCleared (pivot of a dim-1 column: clearing);
+    // the dim-2 pass reads and overwrites every triangle entry of the complex.
+    static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint32 [C(64,3)] triangles
+    static constexpr int64_t mincof_e = mincof + 4 * (64 * 63 * 62 / 6);  // uint32 [C(64,2)] edges
+    static constexpr int64_t edges = mincof_e + 4 * (64 * 63 / 2);   // uint16 [C(64,2)] (i << 8 | j)
+    static constexpr int64_t total = edges + 2 * (64 * 63 / 2);
 };
 
 template <int NP>
 struct BettiSmem {
-    float Dt[NP * (NP - 1) / 2];  // f32 distances, strict lower triangle: (i > j) at i(i-1)/2 + j
+    static constexpr int S = NP + 1;  // odd row stride: row and column reads are conflict-free
+    float D[NP * S];                  // full symmetric f32 distance matrix, D[i * S + j]
     uint64_t adj[NP];
-    uint64_t tree[NP];
-    uint16_t edges[NP * (NP - 1) / 2];
-    uint32_t cleared[(NP * (NP - 1) * (NP - 2) / 6 + 31) / 32];
-    union {
-        struct {
-            double X[NP][3];
-            double sq[NP];
-        } cloud;
-    } u;
-    uint32_t vstore[kVStoreLds];
     float d0[NP];
+    uint8_t par[NP];                  // minimum spanning forest: parent of each vertex (0xFF = root)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -207,26 +203,33 @@ struct Complex {
     } while (0)
 #endif
 
-    __device__ float dlow(int a, int b) const { return s.Dt[c2(a) + b]; }  // a > b
-    __device__ float dist(int i, int j) const {                              // i != j
-        const int a = i > j ? i : j, b = i > j ? j : i;
-        return s.Dt[c2(a) + b];
-    }
+    // Distances are non-negative floats, so their order is the order of their bit patterns:
+    // maxima are taken as unsigned integer maxima (no NaN canonicalization). The matrix is
+    // stored full, so a lookup is one multiply-add whichever vertex is larger.
+    static constexpr int S = BettiSmem<NP>::S;
+    __device__ const uint32_t* Db() const { return reinterpret_cast<const uint32_t*>(s.D); }
+    __device__ uint32_t dlowb(int a, int b) const { return Db()[a * S + b]; }
+    __device__ uint32_t db(int i, int j) const { return Db()[i * S + j]; }
+    __device__ float dlow(int a, int b) const { return __uint_as_float(dlowb(a, b)); }
+    __device__ float dist(int i, int j) const { return __uint_as_float(db(i, j)); }
     __device__ uint64_t ekey(int i, int j) const {  // i != j
-        const int a = i > j ? i : j, b = i > j ? j : i;
-        return make_key(s.Dt[c2(a) + b], pack2(a, b));
+        const int a = max(i, j), b = min(i, j);
+        return make_key(dlow(a, b), pack2(a, b));
     }
-    __device__ float tri_diam(int a, int b, int c) const {  // a > b > c
-        return fmaxf(fmaxf(dlow(a, b), dlow(a, c)), dlow(b, c));
+    __device__ uint32_t tri_diamb(int a, int b, int c) const {  // a > b > c
+        return max(max(dlowb(a, b), dlowb(a, c)), dlowb(b, c));
     }
+    __device__ float tri_diam(int a, int b, int c) const { return __uint_as_float(tri_diamb(a, b, c)); }
     __device__ uint64_t tkey(int a, int b, int c) const { return make_key(tri_diam(a, b, c), pack3(a, b, c)); }
+    // tree edge (i, j): one is the other's parent in the spanning forest
+    __device__ bool is_tree(int i, int j) const { return s.par[i] == j || s.par[j] == i; }
+    // clearing marks live in the triangle min-cofacet table (scratch) until the dim-2 pass
     __device__ bool is_cleared(int a, int b, int c) const {
-        const int t = tri_dense(a, b, c);
-        return (s.cleared[t >> 5] >> (t & 31)) & 1u;
+        return sp<uint32_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] == kCleared;
     }
-    __device__ void set_cleared(int a, int b, int c) {
-        const int t = tri_dense(a, b, c);
-        atomicOr(&s.cleared[t >> 5], 1u << (t & 31));
+    __device__ void set_cleared(int a, int b, int c) { sp<uint32_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] = kCleared; }
+    __device__ uint32_t* mincof_of(int dim) const {
+        return sp<uint32_t>(dim == 1 ? ScratchLayout::mincof_e : ScratchLayout::mincof);
     }
     template <typename T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scratch + off); }
@@ -250,18 +253,48 @@ struct Complex {
     // and ends the search. Cofacets seen before it have larger diameters.
     __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, float diam, uint64_t cand) const {
         uint64_t best = kInf;
+        const uint32_t dbits = __float_as_uint(diam);
+        const uint32_t abc = dim == 1 ? pack2(a, b) : pack3(a, b, c);
+        // four candidates per step (descending), their distance reads issued together
         while (cand) {
-            const int k = 63 - __clzll((long long)cand);
-            cand &= ~(1ull << k);
-            float dk = fmaxf(dist(a, k), dist(b, k));
-            if (dim == 2) dk = fmaxf(dk, dist(c, k));
-            const uint32_t pk = dim == 1 ? tri_with(a, b, k) : tet_with(a, b, c, k);
-            if (dk <= diam) {
-                best = make_key(diam, pk);
-                break;
+            int kk[4];
+            bool val[4];
+            uint32_t dk[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                val[j] = cand != 0;
+                kk[j] = val[j] ? 63 - __clzll((long long)cand) : 0;
+                cand &= ~(1ull << kk[j]) | (val[j] ? 0ull : ~0ull);
             }
-            const uint64_t key = make_key(dk, pk);
-            best = key < best ? key : best;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = kk[j];
+                dk[j] = max(db(a, k), db(b, k));
+                if (dim == 2) dk[j] = max(dk[j], db(c, k));
+            }
+            bool found = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t uk = (uint32_t)kk[j];
+                uint32_t pk;
+                if (dim == 1) {
+                    const uint32_t p1 = pin((uk << 16) | abc);
+                    const uint32_t p2 = pin(((uint32_t)a << 16) | (uk << 8) | (uint32_t)b);
+                    const uint32_t p3 = pin((abc << 8) | uk);
+                    pk = kk[j] > a ? p1 : (kk[j] > b ? p2 : p3);
+                } else {
+                    const uint32_t p1 = pin((uk << 24) | abc);
+                    const uint32_t p2 = pin(((uint32_t)a << 24) | (uk << 16) | (abc & 0xFFFFu));
+                    const uint32_t p3 = pin(((abc >> 8) << 16) | (uk << 8) | (uint32_t)c);
+                    const uint32_t p4 = pin((abc << 8) | uk);
+                    pk = kk[j] > a ? p1 : (kk[j] > b ? p2 : (kk[j] > c ? p3 : p4));
+                }
+                const bool hit = val[j] && !found && dk[j] <= dbits;
+                const uint64_t key = ((uint64_t)(hit ? dbits : dk[j]) << 32) | (uint64_t)(~pk);
+                best = (val[j] && !found && key < best) ? key : best;
+                found = found || hit;
+            }
+            if (found) break;
         }
         return best;
     }
@@ -277,9 +310,8 @@ struct Complex {
         return wave_min_u64(key);
     }
 
-    // F-max facet of pivot tau as (packed vertices); owner iff it is a column (not a tree edge,
-    // not cleared) whose F-min cofacet is tau (apparent pair)
-    __device__ uint32_t max_facet(int dim, uint64_t tau, bool& is_column) const {
+    // F-max facet of pivot tau as (packed vertices)
+    __device__ uint32_t max_facet(int dim, uint64_t tau) const {
         const uint32_t p = key_packed(tau);
         if (dim == 1) {
             const int a = (p >> 16) & 255, b = (p >> 8) & 255, c = p & 255;
@@ -289,7 +321,6 @@ struct Complex {
             if (k > best) { best = k; fa = a; fb = c; }
             k = ekey(b, c);
             if (k > best) { best = k; fa = b; fb = c; }
-            is_column = !((s.tree[fa] >> fb) & 1ull);
             return pack2(fa, fb);
         } else {
             const int a = (p >> 24) & 255, b = (p >> 16) & 255, c = (p >> 8) & 255, d = p & 255;
@@ -301,26 +332,16 @@ struct Complex {
             if (k > best) { best = k; fa = a; fb = c; fc = d; }
             k = tkey(b, c, d);
             if (k > best) { best = k; fa = b; fb = c; fc = d; }
-            is_column = !is_cleared(fa, fb, fc);
             return pack3(fa, fb, fc);
         }
     }
     // Apparent owner of pivot tau (whole wave, uniform): its F-max facet f, if tau is f's
-    // F-minimal cofacet (recorded for every column by the lane-parallel pass), else kNone.
+    // F-minimal cofacet (recorded for every column by the lane-parallel pass; tree edges and
+    // cleared triangles hold kNone), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
-        bool col;
-        const uint32_t f = uni(max_facet(dim, uni64(tau), col));
-#ifdef DGN_APP_FLY
-        if (!uni(col)) return kNone;
-        const int a = (f >> 16) & 255, b = (f >> 8) & 255, c = f & 255;
-        uint64_t mk;
-        if (dim == 1) mk = min_cofacet_wave(1, b, c, 0, dlow(b, c), uni64(s.adj[b]) & uni64(s.adj[c]));
-        else mk = min_cofacet_wave(2, a, b, c, tri_diam(a, b, c), uni64(s.adj[a]) & uni64(s.adj[b]) & uni64(s.adj[c]));
-        return mk == uni64(tau) ? f : kNone;
-#else
-        const uint32_t m = sp<uint32_t>(ScratchLayout::mincof)[col_dense(dim, f)];
+        const uint32_t f = uni(max_facet(dim, uni64(tau)));
+        const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
         return uni(m) == key_packed(tau) ? f : kNone;
-#endif
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {
@@ -427,12 +448,10 @@ struct Complex {
         const int c = (int)(sp_ & 255);
         const bool on = dim == 1 ? ((myadj >> a) & (myadj >> b) & 1ull) != 0
                                  : ((myadj >> a) & (myadj >> b) & (myadj >> c) & 1ull) != 0;
-        // every arm is materialized (pin) so the selects stay v_cndmask, never exec branches
-        const int msk = -(int)on;
-        const int ha = max(k, a), la = min(k, a), hb = max(k, b), lb = min(k, b);
-        const int ia = pin(((ha * (ha - 1)) >> 1) + la) & msk;
-        const int ib = pin(((hb * (hb - 1)) >> 1) + lb) & msk;
-        float dd = fmaxf(diam, fmaxf(s.Dt[ia], s.Dt[ib]));
+        // lane k reads row entries (x, k): consecutive lanes, consecutive banks. Lanes with
+        // k >= NP read past the matrix into adj/tree (still inside the struct) and are masked
+        // off by `on`. Every select arm is materialized (pin): v_cndmask, never exec branches.
+        uint32_t dd = max(__float_as_uint(diam), max(Db()[a * S + k], Db()[b * S + k]));
         uint32_t pk;
         const uint32_t uk = (uint32_t)k;
         if (dim == 1) {
@@ -443,9 +462,7 @@ struct Complex {
             const uint32_t p3 = pin((ab << 8) | uk);
             pk = k > a ? p1 : (k > b ? p2 : p3);
         } else {
-            const int hc = max(k, c), lc = min(k, c);
-            const int ic = pin(((hc * (hc - 1)) >> 1) + lc) & msk;
-            dd = fmaxf(dd, s.Dt[ic]);
+            dd = max(dd, Db()[c * S + k]);
             const uint32_t abc = sp_ & 0xFFFFFFu;
             const uint32_t p1 = pin((uk << 24) | abc);
             const uint32_t p2 = pin(((uint32_t)a << 24) | (uk << 16) | (abc & 0xFFFFu));
@@ -453,7 +470,7 @@ struct Complex {
             const uint32_t p4 = pin((abc << 8) | uk);
             pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
         }
-        const uint64_t key = make_key(dd, pk);
+        const uint64_t key = ((uint64_t)dd << 32) | (uint64_t)(~pk);
         return (on && key > floor) ? key : kInf;
     }
 
@@ -495,9 +512,8 @@ struct Complex {
     // per-lane apparent owner of pivot tau (kNone if none): its F-max facet f, if tau is f's
     // F-minimal cofacet (recorded for every column by the lane-parallel pass)
     __device__ uint32_t apparent_owner_lane(int dim, uint64_t tau) const {
-        bool col;
-        const uint32_t f = max_facet(dim, tau, col);
-        const uint32_t m = sp<uint32_t>(ScratchLayout::mincof)[col_dense(dim, f)];
+        const uint32_t f = max_facet(dim, tau);
+        const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
         return m == key_packed(tau) ? f : kNone;
     }
 
@@ -598,9 +614,13 @@ struct Complex {
                             ok = v_toggle(dim, m & ~kLazyBit, v);
                         } else {
                             const int off = (int)uni(m >> 9), len = (int)uni(m & 511);
-                            for (int t = 0; t < len && ok; ++t) {
-                                const uint32_t x = uni(off + t < kVStoreLds ? s.vstore[off + t] : gvstore[off + t]);
-                                ok = v_toggle(dim, x, v);
+                            // owner's V list: one lane-parallel load per 64 entries, then readlanes
+                            for (int t0 = 0; t0 < len && ok; t0 += kWave) {
+                                const int t = t0 + lane;
+                                uint32_t w = 0;
+                                if (t < len) w = gvstore[off + t];
+                                const int cnt = len - t0 < kWave ? len - t0 : kWave;
+                                for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(dim, rl(w, u), v);
                             }
                         }
                     }
@@ -646,8 +666,7 @@ struct Complex {
                 if (vused + v > kVStoreCap || v > 511) { err |= kErrR; return; }
                 for (int t = lane; t < v; t += kWave) {
                     const uint32_t x = t < kWave ? vs0 : vs1;
-                    if (vused + t < kVStoreLds) s.vstore[vused + t] = x;
-                    else gvstore[vused + t] = x;
+                    gvstore[vused + t] = x;
                 }
                 meta = ((uint32_t)vused << 9) | (uint32_t)v;
                 vused = (int)uni((uint32_t)(vused + v));
@@ -695,14 +714,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
         if (chunk0 >= total) break;
         for (int64_t wi = chunk0; wi < chunk0 + kChunk && wi < total; ++wi) {
             const int64_t gi = bl.work_list ? (int64_t)bl.work_list[wi] : wi;
-            int64_t r0 = 0;
-            int n;
-            if (bl.clouds || bl.lower) {
-                n = bl.npoints[gi];
-            } else {
-                r0 = bl.row_ptr[gi];
-                n = (int)(bl.row_ptr[gi + 1] - r0) + 1;
-            }
+            const int n = bl.npoints[gi];
             double* feat = bl.features ? bl.features + 35 * gi : nullptr;
             if (n > NP) {
                 if (bl.skip_above) continue;  // reduced by the overflow launch
@@ -711,22 +723,8 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
                 continue;
             }
-            // structure of gi and the 1/count weight (betti_features.cpp:62-63, 77)
-            double weight = 1.0;
-            if (bl.species) {
-                int64_t lo = 0, hi = bl.num_structures - 1;
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi + 1) >> 1;
-                    if (bl.atom_offset[mid] <= gi) lo = mid;
-                    else hi = mid - 1;
-                }
-                const int64_t s0 = bl.atom_offset[lo], s1 = bl.atom_offset[lo + 1];
-                const int spc = bl.species[gi];
-                int cnt = 0;
-                for (int64_t j = s0 + lane; j < s1; j += kWave) cnt += (bl.species[j] == spc);
-                cnt = wave_sum(cnt);
-                weight = 1.0 / (double)cnt;
-            }
+            // 1/count(species) weight (betti_features.cpp:62-63, 77), from the distance pass
+            const double weight = bl.weight ? bl.weight[gi] : 1.0;
 
             Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0, 0, 0};
 #ifdef DGN_PHASE_TIMING
@@ -734,76 +732,30 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             cx.tprev = &t_prev;
 #endif
             DGN_PHASE(7);
-            // ---- load the local cloud (betti_features.cpp:67-73) ----
-            if (lane < n && bl.clouds) {
-                const double* xc = bl.clouds + ((int64_t)gi * bl.cloud_stride + lane) * 3;
-                s.u.cloud.X[lane][0] = xc[0];
-                s.u.cloud.X[lane][1] = xc[1];
-                s.u.cloud.X[lane][2] = xc[2];
-                s.u.cloud.sq[lane] = (xc[0] * xc[0] + xc[1] * xc[1]) + xc[2] * xc[2];
-            } else if (lane < n && !bl.lower) {
-                const double* q = bl.pos + 3 * gi;
-                double x[3];
-                if (lane == 0) {
-                    x[0] = q[0]; x[1] = q[1]; x[2] = q[2];
-                } else {
-                    const double* dv = bl.disp + 3 * (r0 + lane - 1);
-                    x[0] = q[0] + dv[0]; x[1] = q[1] + dv[1]; x[2] = q[2] + dv[2];
-                }
-                s.u.cloud.X[lane][0] = x[0];
-                s.u.cloud.X[lane][1] = x[1];
-                s.u.cloud.X[lane][2] = x[2];
-                // rowwise().squaredNorm(): (x0^2 + x1^2) + x2^2
-                s.u.cloud.sq[lane] = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
-            }
-            lds_sync();
-            // ---- distance matrix on the matrix cores (ripser_wrapper.cpp:64-67) ----
-            if (bl.lower) {
-                // given f32 lower triangle (ripser_wrapper.cpp:20-24 packing)
-                const float* L = bl.lower + (int64_t)gi * ((int64_t)bl.cloud_stride * (bl.cloud_stride - 1) / 2);
-                const int tot = n * (n - 1) / 2;
-                for (int t = lane; t < tot; t += kWave) s.Dt[t] = L[t];  // same packing
-            } else {
-                typedef double double4_t __attribute__((ext_vector_type(4)));
-                const int T = (n + 15) / 16;
-                const int kk = lane >> 4;
-                for (int I = 0; I < T; ++I) {
-                    for (int J = 0; J <= I; ++J) {
-                        const int ra = 16 * I + (lane & 15);
-                        const int cb = 16 * J + (lane & 15);
-                        const double xa = (ra < n && kk < 3) ? s.u.cloud.X[ra][kk] : 0.0;
-                        const double xb = (cb < n && kk < 3) ? s.u.cloud.X[cb][kk] : 0.0;
-                        const double4_t z = {0.0, 0.0, 0.0, 0.0};
-                        // rank-1 products: operand k' nonzero only for k' == k -> round(x_ik * x_jk)
-                        const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 0 ? xa : 0.0, kk == 0 ? xb : 0.0, z, 0, 0, 0);
-                        const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 1 ? xa : 0.0, kk == 1 ? xb : 0.0, z, 0, 0, 0);
-                        const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 2 ? xa : 0.0, kk == 2 ? xb : 0.0, z, 0, 0, 0);
-                        const int col = 16 * J + (lane & 15);
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int row = 16 * I + (lane >> 4) + 4 * r;
-                            if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
-                                const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
-                                const double d2 = (s.u.cloud.sq[row] + s.u.cloud.sq[col]) - 2.0 * dot;
-                                s.Dt[c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
-                            }
-                        }
+            constexpr int S = BettiSmem<NP>::S;
+            {
+                // f32 strict lower triangle (ripser_wrapper.cpp:20-24 packing), mirrored into
+                // the full matrix; one coalesced read per row
+                const float* L = bl.lower + gi * bl.tri_stride;
+                for (int i = 1; i < n; ++i)
+                    if (lane < i) {
+                        const float d = L[c2(i) + lane];
+                        s.D[i * S + lane] = d;
+                        s.D[lane * S + i] = d;
                     }
-                }
             }
             lds_sync();
             DGN_PHASE(0);
             // ---- adjacency (sparse_distance_matrix: i != j and d <= thr, ripser.cpp:386-395) ----
             {
                 uint64_t m = 0;
-                if (lane < n) {
-                    for (int w2 = 0; w2 < n; ++w2)
-                        if (w2 != lane && cx.dist(lane, w2) <= cx.thr) m |= 1ull << w2;
+                for (int i = 0; i < n; ++i) {
+                    const uint64_t row = ballot(lane < n && lane != i && s.D[i * S + lane] <= cx.thr);
+                    if (lane == i) m = row;
                 }
                 s.adj[lane] = lane < n ? m : 0ull;
-                s.tree[lane] = 0ull;
+                if (lane < NP) s.par[lane] = 0xFF;
             }
-            for (int i = lane; i < (int)(sizeof(s.cleared) / 4); i += kWave) s.cleared[i] = 0u;
             lds_sync();
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
@@ -833,10 +785,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                             if (lane == 0) s.d0[cx.n_d0] = dd;
                             cx.n_d0 += 1;
                         }
-                        if (lane == 0) {
-                            s.tree[u] |= 1ull << v;
-                            s.tree[v] |= 1ull << u;
-                        }
+                        if (lane == 0) s.par[v] = (uint8_t)u;
                     }
                     if (lane == v) in_tree = true;
                     ++added;
@@ -848,6 +797,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             }
             lds_sync();
             // ---- edge list (i > j, d <= thr), row-major ----
+            uint16_t* edges = cx.template sp<uint16_t>(ScratchLayout::edges);
             int n_edges = 0;
             {
                 const uint64_t low = lane < n ? (s.adj[lane] & ((lane == 0) ? 0ull : ((1ull << lane) - 1ull))) : 0ull;
@@ -859,16 +809,17 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 while (mm) {
                     const int j = __ffsll((unsigned long long)mm) - 1;
                     mm &= mm - 1;
-                    s.edges[off++] = (uint16_t)((lane << 8) | j);
+                    edges[off++] = (uint16_t)((lane << 8) | j);
                 }
             }
-            lds_sync();
+            __syncthreads();  // edge list (global scratch) visible to every lane
             cx.n_p1 = 0;
             cx.n_p2 = 0;
             DGN_PHASE(1);
             uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
             uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
             uint32_t* mincof = cx.template sp<uint32_t>(ScratchLayout::mincof);
+            uint32_t* mincof_e = cx.template sp<uint32_t>(ScratchLayout::mincof_e);
                     // ---- dim 1: one lane per column (non-tree edge) ----
             if (dim_max >= 1) {
                 int nna = 0;
@@ -878,18 +829,18 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                     float birth = 0.f, death = 0.f;
                     uint64_t colkey = 0, best = kInf;
                     if (e < n_edges) {
-                        const int i = s.edges[e] >> 8, j = s.edges[e] & 255;
+                        const uint32_t ed = edges[e];
+                        const int i = ed >> 8, j = ed & 255;
                         uint32_t mc = kNone;
-                        if (!((s.tree[i] >> j) & 1ull)) {
+                        if (!cx.is_tree(i, j)) {
                             birth = cx.dlow(i, j);
                             colkey = make_key(birth, pack2(i, j));
                             const uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
                                 best = cx.min_cofacet_lane(1, i, j, 0, birth, cand);
                                 death = key_diam(best);
-                                bool col_unused;
                                 // apparent iff (i,j) is the F-max facet of its pivot triangle
-                                apparent = cx.max_facet(1, best, col_unused) == pack2(i, j);
+                                apparent = cx.max_facet(1, best) == pack2(i, j);
                                 if (apparent) {
                                     const uint32_t tp = key_packed(best);
                                     cx.set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
@@ -899,7 +850,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                                 mc = key_packed(best);
                             }
                         }
-                        mincof[edge_dense(i, j)] = mc;
+                        mincof_e[edge_dense(i, j)] = mc;
                     }
                     cx.append_pairs(1, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
@@ -919,11 +870,16 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 const int a0 = cx.n_adds;
 #endif
                 cx.reduce_serial(1, nna);
-                lds_sync();
+                __syncthreads();  // clearing marks (scratch stores) complete before the dim-2 pass
                 DGN_PHASE(3);
 #ifdef DGN_PHASE_TIMING
                 ph[10] += cx.n_adds - a0;
 #endif
+            }
+            if (!(dim_max >= 2 && cx.err == 0) && n >= 3) {
+                // no dim-2 pass to consume them: erase every triangle entry (clearing marks)
+                for (int t = lane; t < c3(n); t += kWave) mincof[t] = kNone;
+                __syncthreads();
             }
             // ---- dim 2: one lane per column (uncleared triangle) ----
             if (dim_max >= 2 && cx.err == 0) {
@@ -939,8 +895,9 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                         if (!bal || next_edge >= n_edges) break;
                         const int e = next_edge + mask_prefix(bal);
                         if (need && e < n_edges) {
-                            ea = s.edges[e] >> 8;
-                            eb = s.edges[e] & 255;
+                            const uint32_t ed = edges[e];
+                            ea = ed >> 8;
+                            eb = ed & 255;
                             tmask = s.adj[ea] & s.adj[eb] & ((1ull << eb) - 1ull);
                         }
                         next_edge += __popcll(bal);
@@ -963,9 +920,8 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                             if (cand) {
                                 best = cx.min_cofacet_lane(2, a, b, c, birth, cand);
                                 death = key_diam(best);
-                                bool col_unused;
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
-                                apparent = cx.max_facet(2, best, col_unused) == pack3(a, b, c);
+                                apparent = cx.max_facet(2, best) == pack3(a, b, c);
                                 na_col = !apparent;
                                 mc = key_packed(best);
                             }
@@ -1009,6 +965,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
             // group g: 0 d0 death | 1..3 d1 pers, birth, death | 4..6 d2 pers, birth, death
             double myval = 0.0;
+#pragma unroll 1
             for (int g = 0; g < 7; ++g) {
                 const int m = g == 0 ? cx.n_d0 : (g <= 3 ? cx.n_p1 : cx.n_p2);
                 double st[5] = {0, 0, 0, 0, 0};
@@ -1082,6 +1039,108 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Local distance matrices on the matrix cores (ripser_wrapper.cpp:60-70 + 17-24).
+// One wave per complex: cloud row 0 = pos_i, row k = pos_i + disp_k (betti_features.cpp:67-73)
+// or a caller-given cloud; the K = 3 Gram product as three rank-1 v_mfma_f64_16x16x4_f64
+// (each exactly round(x_ik * x_jk)) summed (p0 + p1) + p2 on the VALU, then
+// sqrt(max(0, (sq_i + sq_j) - 2 dot)) -> f32: bit-identical to the reference's Eigen path.
+// Writes the strict lower triangle in the reference's packing (row i, j < i at i(i-1)/2 + j),
+// the point count and the 1/count(species) weight of each complex.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLaunch dl) {
+    __shared__ double sq_s[4][64];
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    double* sq = sq_s[w];
+    typedef double double4_t __attribute__((ext_vector_type(4)));
+    for (int64_t c = (int64_t)blockIdx.x * 4 + w; c < dl.count; c += (int64_t)gridDim.x * 4) {
+        const int64_t gi = dl.first + c;
+        int64_t r0 = 0;
+        int n;
+        if (bl.clouds) {
+            n = bl.npoints[gi];
+        } else {
+            r0 = bl.row_ptr[gi];
+            n = (int)(bl.row_ptr[gi + 1] - r0) + 1;
+        }
+        if (lane == 0) dl.npoints[c] = n;
+        // 1/count(species) of the centre's structure (betti_features.cpp:62-63, 77)
+        if (bl.species) {
+            int64_t lo = 0, hi = bl.num_structures - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi + 1) >> 1;
+                if (bl.atom_offset[mid] <= gi) lo = mid;
+                else hi = mid - 1;
+            }
+            const int64_t s0 = bl.atom_offset[lo], s1 = bl.atom_offset[lo + 1];
+            const int spc = bl.species[gi];
+            int cnt = 0;
+            for (int64_t j = s0 + lane; j < s1; j += kWave) cnt += (bl.species[j] == spc);
+            cnt = wave_sum(cnt);
+            if (lane == 0) dl.weight[c] = 1.0 / (double)cnt;
+        } else if (lane == 0) {
+            dl.weight[c] = 1.0;
+        }
+        if (n > 64) continue;  // the Betti pass flags it
+        // lane p holds cloud row p; all loads issued together
+        const int pl = lane < n ? lane : n - 1;
+        double px[3];
+        if (bl.clouds) {
+            const double* xc = bl.clouds + ((int64_t)gi * bl.cloud_stride + pl) * 3;
+            px[0] = xc[0]; px[1] = xc[1]; px[2] = xc[2];
+        } else {
+            const double* q = bl.pos + 3 * gi;
+            const double* dv = bl.disp + 3 * (r0 + (pl > 0 ? pl - 1 : 0));
+            const double d0v = dv[0], d1v = dv[1], d2v = dv[2];
+            px[0] = pl == 0 ? q[0] : q[0] + d0v;
+            px[1] = pl == 0 ? q[1] : q[1] + d1v;
+            px[2] = pl == 0 ? q[2] : q[2] + d2v;
+        }
+        sq[lane] = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
+        const int T = (n + 15) / 16;
+        const int kk = lane >> 4;
+        double xr[4];  // coordinate kk of cloud row 16 I + (lane & 15)
+#pragma unroll
+        for (int I = 0; I < 4; ++I) {
+            const int ra = 16 * I + (lane & 15);
+            const double v0 = __shfl(px[0], ra, kWave), v1 = __shfl(px[1], ra, kWave), v2 = __shfl(px[2], ra, kWave);
+            xr[I] = (ra < n && kk < 3) ? (kk == 0 ? v0 : (kk == 1 ? v1 : v2)) : 0.0;
+        }
+        float* L = dl.lower + c * bl.tri_stride;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int I = 0; I < T; ++I) {
+            for (int J = 0; J <= I; ++J) {
+                const double xa = I == 0 ? xr[0] : (I == 1 ? xr[1] : (I == 2 ? xr[2] : xr[3]));
+                const double xb = J == 0 ? xr[0] : (J == 1 ? xr[1] : (J == 2 ? xr[2] : xr[3]));
+                const double4_t z = {0.0, 0.0, 0.0, 0.0};
+                // rank-1 products: operand k' nonzero only for k' == k -> round(x_ik * x_jk)
+                const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 0 ? xa : 0.0, kk == 0 ? xb : 0.0, z, 0, 0, 0);
+                const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 1 ? xa : 0.0, kk == 1 ? xb : 0.0, z, 0, 0, 0);
+                const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 2 ? xa : 0.0, kk == 2 ? xb : 0.0, z, 0, 0, 0);
+                const int col = 16 * J + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = 16 * I + (lane >> 4) + 4 * r;
+                    if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
+                        const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
+                        const double d2 = (sq[row] + sq[col]) - 2.0 * dot;
+                        L[c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+}
+
+hipError_t launch_betti_dist(hipStream_t st, const BettiLaunch& b, const DistLaunch& d) {
+    if (d.count <= 0) return hipSuccess;
+    int64_t blocks = (d.count + 3) / 4;
+    if (blocks > 256 * 64) blocks = 256 * 64;
+    hipLaunchKernelGGL(betti_dist_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, d);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 int betti_max_points() { return 64; }
 int64_t betti_scratch_bytes_per_wave() { return ScratchLayout::total; }
 
@@ -1102,7 +1161,7 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int n = 0;
     if (gi < bl.num_atoms)
-        n = (bl.clouds || bl.lower) ? bl.npoints[gi] : (int)(bl.row_ptr[gi + 1] - bl.row_ptr[gi]) + 1;
+        n = bl.npoints[gi];
     const bool big = gi < bl.num_atoms && n > np_small;
     const uint64_t bal = ballot(big);
     if (!bal) return;

@@ -87,7 +87,7 @@ struct dgn_ctx {
     int64_t cnt_edges = 0;
     double cnt_sum_sq = 0;
     // betti workspace
-    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list;
+    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w;
     int betti_slots = 0;
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
@@ -340,7 +340,6 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.scratch = c->b_scratch.as<uint8_t>();
     bl.scratch_per_wave = spw;
     bl.clouds = clouds;
-    bl.lower = lower;
     bl.npoints = npoints;
     bl.cloud_stride = cloud_stride;
     bl.pairs_out = pairs_out;
@@ -350,13 +349,55 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
     bl.phase_cycles = c->phase.as<unsigned long long>();
 #endif
-    {
-        // algorithmic bytes: CSR rows in (disp 24 B/edge + row_ptr) + positions + 35 f64 + 4 i32 out;
-        // flops: 6 n^2 per complex for the Gram product is accounted in DESIGN.md, not here
-        const double bytes = given ? 0.0 : ((double)c->cnt_edges * 24 + (double)A * (8 + 24 + 4 + 35 * 8 + 16));
-        // useful flops of the local Gram product: 6 n^2 per complex
-        TimedLaunch t(c, "betti_vr", bytes, given ? 0.0 : 6.0 * c->cnt_sum_sq);
-        HIP_TRY(c, launch_betti(c->stream, bl, max_points, c->betti_slots));
+    // Betti pass over complexes [c0, c0 + cnt) whose triangles are in `lower`
+    auto vr_pass = [&](int64_t c0, int64_t cnt, const float* tri, int64_t tri_stride, const int32_t* np,
+                       const double* w, double bytes) -> int {
+        BettiLaunch pb = bl;
+        pb.lower = tri;
+        pb.npoints = np;
+        pb.weight = w;
+        pb.tri_stride = tri_stride;
+        pb.num_atoms = cnt;
+        pb.features = features ? features + 35 * c0 : nullptr;
+        pb.counts = counts ? counts + 4 * c0 : nullptr;
+        pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
+        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 3 * sizeof(uint32_t), c->stream));
+        TimedLaunch t(c, "betti_vr", bytes, 0.0);
+        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots));
+        return DGN_OK;
+    };
+    if (lower) {
+        // caller-given triangles: the Betti pass alone
+        int st = vr_pass(0, A, lower, (int64_t)cloud_stride * (cloud_stride - 1) / 2, npoints, nullptr, 0.0);
+        if (st) return st;
+    } else {
+        // distance pass (MFMA) + Betti pass per chunk of complexes; the triangle buffer is
+        // bounded (~4 GB) so arbitrarily large shards stream through it
+        const int64_t tri_stride = std::max<int64_t>(1, (int64_t)max_points * (max_points - 1) / 2);
+        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(4) << 30) / (4 * tri_stride)));
+        bl.tri_stride = tri_stride;  // the distance pass writes [chunk][tri_stride]
+        HIP_TRY(c, c->b_lower.ensure(sizeof(float) * (size_t)(chunk * tri_stride)));
+        HIP_TRY(c, c->b_np.ensure(sizeof(int32_t) * (size_t)chunk));
+        HIP_TRY(c, c->b_w.ensure(sizeof(double) * (size_t)chunk));
+        // per-complex averages over the batch: points n (sum n = E + A), sum n^2 from the count pass
+        const double En = given ? 0.0 : (double)c->cnt_edges, An = (double)A;
+        const double sum_n2 = given ? 0.0 : c->cnt_sum_sq;
+        for (int64_t c0 = 0; c0 < A; c0 += chunk) {
+            const int64_t cnt = std::min<int64_t>(chunk, A - c0);
+            const double f = (double)cnt / An;
+            DistLaunch dl{c0, cnt, c->b_lower.as<float>(), c->b_np.as<int32_t>(), c->b_w.as<double>()};
+            {
+                // algorithmic bytes: displacements + row_ptr + centre position in, triangles (4 C(n,2))
+                // + point count + weight out; useful flops 6 n^2 per complex
+                const double bytes = given ? 0.0 : f * (24 * En + 8 * An + 24 * An + 2 * (sum_n2 - (En + An)) + 12 * An);
+                TimedLaunch t(c, "betti_dist", bytes, given ? 0.0 : f * 6.0 * sum_n2);
+                HIP_TRY(c, launch_betti_dist(c->stream, bl, dl));
+            }
+            // Betti pass: triangles in, 35 f64 + 4 i32 out
+            const double bytes = given ? 0.0 : f * (2 * (sum_n2 - (En + An)) + 12 * An + An * (35 * 8 + 16));
+            int st = vr_pass(c0, cnt, c->b_lower.as<float>(), tri_stride, c->b_np.as<int32_t>(), c->b_w.as<double>(), bytes);
+            if (st) return st;
+        }
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
                               c->stream));

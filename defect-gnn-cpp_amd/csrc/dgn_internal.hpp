@@ -80,10 +80,13 @@ struct BettiLaunch {
     int64_t scratch_per_wave;
     // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
     const double* clouds;
-    // optional distance-input mode (dgn_host_persistence_lower): lower[c][stride*(stride-1)/2] f32
+    // Betti pass input: lower[c][tri_stride] f32 strict lower triangles (from betti_dist_kernel
+    // or caller-given, dgn_host_persistence_lower), npoints[c], optional weight[c]
     const float* lower;
     const int32_t* npoints;
-    int32_t cloud_stride;     // max_points
+    const double* weight;     // 1/count(species) per complex (null = 1)
+    int64_t tri_stride;       // floats per complex in `lower`
+    int32_t cloud_stride;     // max_points (cloud-input mode row stride)
     // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
     float* pairs_out;
     int32_t pair_cap;
@@ -93,6 +96,14 @@ struct BettiLaunch {
     uint32_t* queue;          // work counter of this launch
     int32_t skip_above;       // 1 = complexes above NP are left to the overflow launch
 };
+// distance pass over complexes [first, first + count) of a BettiLaunch's CSR / cloud input
+struct DistLaunch {
+    int64_t first, count;
+    float* lower;      // [count][tri_stride]
+    int32_t* npoints;  // [count]
+    double* weight;    // [count]
+};
+hipError_t launch_betti_dist(hipStream_t s, const BettiLaunch& b, const DistLaunch& d);
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();
 int betti_grid_waves(int device);
