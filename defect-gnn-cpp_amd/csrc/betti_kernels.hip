@@ -42,7 +42,10 @@ constexpr int kChunk = 4;         // complexes per dequeue
 constexpr uint64_t kInf = ~0ull;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr uint32_t kLazyBit = 0x80000000u;  // vmeta: V = {column simplex} (packed in the low bits)
-constexpr uint32_t kCleared = 0xC0000000u;  // mincof triangle mark (no packed tetrahedron has bit 31)
+// min-cofacet table entries (one byte per edge / triangle): the vertex k whose insertion gives
+// the F-minimal cofacet, or one of these marks
+constexpr uint8_t kMcNone = 0xFF;     // not a column, or no cofacet
+constexpr uint8_t kMcCleared = 0xFE;  // triangle is the pivot of a dim-1 column (clearing)
 
 // error bits (mirrored in dgn_api.cpp)
 constexpr uint32_t kErrTooManyPoints = 1u << 0;
@@ -64,13 +67,14 @@ struct ScratchLayout {
     static constexpr int64_t p1 = piv + 8 * kPivCap;                 // float2 [kPairCap]
     static constexpr int64_t p2 = p1 + 8 * kPairCap;                 // float2 [kPairCap]
     static constexpr int64_t vstore = p2 + 8 * kPairCap;             // uint32 [kVStoreCap]
-    // F-minimal cofacet (packed) of every edge / triangle of the complex, indexed by its dense
-    // combinatorial index; kNone for simplices that are not columns or have no cofacet. Before
-    // the dim-2 pass a triangle entry may hold kCleared (pivot of a dim-1 column: clearing);
-    // the dim-2 pass reads and overwrites every triangle entry of the complex.
-    static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint32 [C(64,3)] triangles
-    static constexpr int64_t mincof_e = mincof + 4 * (64 * 63 * 62 / 6);  // uint32 [C(64,2)] edges
-    static constexpr int64_t edges = mincof_e + 4 * (64 * 63 / 2);   // uint16 [C(64,2)] (i << 8 | j)
+    // F-minimal cofacet of every edge / triangle of the complex as the inserted vertex (one
+    // byte), indexed by the dense combinatorial index; kMcNone for simplices that are not
+    // columns or have no cofacet. Before the dim-2 pass a triangle entry may hold kMcCleared;
+    // the dim-2 pass reads and overwrites every triangle entry of the complex. One byte keeps
+    // the per-wave table (C(n,3) B) cache-resident for the serial walk's owner lookups.
+    static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint8 [C(64,3)] triangles
+    static constexpr int64_t mincof_e = mincof + (64 * 63 * 62 / 6);  // uint8 [C(64,2)] edges
+    static constexpr int64_t edges = (mincof_e + (64 * 63 / 2) + 15) / 16 * 16;  // uint16 [C(64,2)] (i << 8 | j)
     static constexpr int64_t total = edges + 2 * (64 * 63 / 2);
 };
 
@@ -161,6 +165,9 @@ __device__ __forceinline__ uint32_t tri_with(int a, int b, int k) {  // a > b; i
 __device__ __forceinline__ uint32_t tet_with(int a, int b, int c, int k) {  // a > b > c; insert k
     return k > a ? pack4(k, a, b, c) : k > b ? pack4(a, k, b, c) : k > c ? pack4(a, b, k, c) : pack4(a, b, c, k);
 }
+// vertex of the packed cofacet `tau` that is not in its packed facet `f` (vertex sums)
+__device__ __forceinline__ uint32_t byte_sum(uint32_t p) { return (p & 255) + ((p >> 8) & 255) + ((p >> 16) & 255) + (p >> 24); }
+__device__ __forceinline__ uint32_t extra_vertex(uint32_t tau, uint32_t f) { return byte_sum(tau) - byte_sum(f); }
 __device__ __forceinline__ int tri_dense(int a, int b, int c) {  // combinatorial index, a > b > c
     return a * (a - 1) * (a - 2) / 6 + b * (b - 1) / 2 + c;
 }
@@ -225,11 +232,11 @@ struct Complex {
     __device__ bool is_tree(int i, int j) const { return s.par[i] == j || s.par[j] == i; }
     // clearing marks live in the triangle min-cofacet table (scratch) until the dim-2 pass
     __device__ bool is_cleared(int a, int b, int c) const {
-        return sp<uint32_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] == kCleared;
+        return sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] == kMcCleared;
     }
-    __device__ void set_cleared(int a, int b, int c) { sp<uint32_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] = kCleared; }
-    __device__ uint32_t* mincof_of(int dim) const {
-        return sp<uint32_t>(dim == 1 ? ScratchLayout::mincof_e : ScratchLayout::mincof);
+    __device__ void set_cleared(int a, int b, int c) { sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] = kMcCleared; }
+    __device__ uint8_t* mincof_of(int dim) const {
+        return sp<uint8_t>(dim == 1 ? ScratchLayout::mincof_e : ScratchLayout::mincof);
     }
     template <typename T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scratch + off); }
@@ -341,7 +348,7 @@ struct Complex {
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         const uint32_t f = uni(max_facet(dim, uni64(tau)));
         const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
-        return uni(m) == key_packed(tau) ? f : kNone;
+        return uni(m) == extra_vertex(key_packed(tau), f) ? f : kNone;
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {
@@ -514,7 +521,7 @@ struct Complex {
     __device__ uint32_t apparent_owner_lane(int dim, uint64_t tau) const {
         const uint32_t f = max_facet(dim, tau);
         const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
-        return m == key_packed(tau) ? f : kNone;
+        return m == extra_vertex(key_packed(tau), f) ? f : kNone;
     }
 
     // Walk the non-apparent columns in Ripser's order (whole wave). na_* (scratch) hold each
@@ -818,8 +825,8 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             DGN_PHASE(1);
             uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
             uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
-            uint32_t* mincof = cx.template sp<uint32_t>(ScratchLayout::mincof);
-            uint32_t* mincof_e = cx.template sp<uint32_t>(ScratchLayout::mincof_e);
+            uint8_t* mincof = cx.template sp<uint8_t>(ScratchLayout::mincof);
+            uint8_t* mincof_e = cx.template sp<uint8_t>(ScratchLayout::mincof_e);
                     // ---- dim 1: one lane per column (non-tree edge) ----
             if (dim_max >= 1) {
                 int nna = 0;
@@ -831,7 +838,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                     if (e < n_edges) {
                         const uint32_t ed = edges[e];
                         const int i = ed >> 8, j = ed & 255;
-                        uint32_t mc = kNone;
+                        uint32_t mc = kMcNone;
                         if (!cx.is_tree(i, j)) {
                             birth = cx.dlow(i, j);
                             colkey = make_key(birth, pack2(i, j));
@@ -847,10 +854,10 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                                 } else {
                                     na_col = true;
                                 }
-                                mc = key_packed(best);
+                                mc = extra_vertex(key_packed(best), pack2(i, j));
                             }
                         }
-                        mincof_e[edge_dense(i, j)] = mc;
+                        mincof_e[edge_dense(i, j)] = (uint8_t)mc;
                     }
                     cx.append_pairs(1, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
@@ -878,7 +885,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             }
             if (!(dim_max >= 2 && cx.err == 0) && n >= 3) {
                 // no dim-2 pass to consume them: erase every triangle entry (clearing marks)
-                for (int t = lane; t < c3(n); t += kWave) mincof[t] = kNone;
+                for (int t = lane; t < c3(n); t += kWave) mincof[t] = kMcNone;
                 __syncthreads();
             }
             // ---- dim 2: one lane per column (uncleared triangle) ----
@@ -912,7 +919,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                         const int a = ea, b = eb;
                         const int c = __ffsll((unsigned long long)tmask) - 1;
                         tmask &= tmask - 1;
-                        uint32_t mc = kNone;
+                        uint32_t mc = kMcNone;
                         if (!cx.is_cleared(a, b, c)) {
                             birth = cx.tri_diam(a, b, c);
                             colkey = make_key(birth, pack3(a, b, c));
@@ -923,10 +930,10 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
                                 apparent = cx.max_facet(2, best) == pack3(a, b, c);
                                 na_col = !apparent;
-                                mc = key_packed(best);
+                                mc = extra_vertex(key_packed(best), pack3(a, b, c));
                             }
                         }
-                        mincof[tri_dense(a, b, c)] = mc;
+                        mincof[tri_dense(a, b, c)] = (uint8_t)mc;
                     }
                     cx.append_pairs(2, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
