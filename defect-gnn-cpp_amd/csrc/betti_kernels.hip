@@ -704,7 +704,9 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
     __shared__ int64_t chunk_s;
 #ifdef DGN_PHASE_TIMING
-    uint64_t ph[32] = {0};
+    // diagnostics counters in LDS (registers would change the kernel's occupancy)
+    __shared__ uint64_t ph[32];
+    if (lane_id() < 32) ph[lane_id()] = 0;
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();

@@ -42,6 +42,6 @@ out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round
        "na1_per_complex": ph[8] / A, "na2_per_complex": ph[9] / A, "adds1": ph[10] / A, "adds2": ph[11] / A,
        "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13],
        "pivot_V_entries_per_complex": ph[14] / A, "pivot_V_sq_per_complex": ph[15] / A,
-       "max_V": ph[23], "pivot_iters_per_complex": ph[24] / A, "pivot_iter_entries_per_complex": ph[25] / A,
+       "max_V": ph[23], "pivot_iters_per_complex": ph[24] / A, "pivot_iter_entries_per_complex": ph[25] / A, "d2_rounds": ph[28] / A, "d2_active_lanes": ph[29] / A, "d2_wave_groups": ph[26] / A, "d2_lane_groups": ph[27] / A,
        "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
 print(json.dumps(out, indent=1))
