@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
 // the point count and the 1/count(species) weight of each complex.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLaunch dl) {
-    __shared__ double sq_s[4][64];
+    __shared__ double sq_s[4][kWideMaxPoints];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     double* sq = sq_s[w];
     typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -1089,7 +1089,46 @@ __global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLau
         } else if (lane == 0) {
             dl.weight[c] = 1.0;
         }
-        if (n > 64) continue;  // the Betti pass flags it
+        if (n > kWideMaxPoints) continue;  // the Betti pass flags it
+        if (n > 64) {
+            // wide complex: rows read straight from global memory, one 16 x 16 tile at a time
+            const int kq = lane >> 4;
+            auto point = [&](int p, int d) -> double {
+                if (bl.clouds) return bl.clouds[((int64_t)gi * bl.cloud_stride + p) * 3 + d];
+                const double q = bl.pos[3 * gi + d];
+                return p == 0 ? q : q + bl.disp[3 * (r0 + p - 1) + d];
+            };
+            for (int p = lane; p < n; p += kWave) {
+                const double x0 = point(p, 0), x1 = point(p, 1), x2 = point(p, 2);
+                sq[p] = (x0 * x0 + x1 * x1) + x2 * x2;  // rowwise().squaredNorm()
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            float* L = dl.lower + c * bl.tri_stride;
+            const int T = (n + 15) / 16;
+            for (int I = 0; I < T; ++I) {
+                const int ra = 16 * I + (lane & 15);
+                const double xa = (ra < n && kq < 3) ? point(ra, kq) : 0.0;
+                for (int J = 0; J <= I; ++J) {
+                    const int cb = 16 * J + (lane & 15);
+                    const double xb = (cb < n && kq < 3) ? point(cb, kq) : 0.0;
+                    const double4_t z = {0.0, 0.0, 0.0, 0.0};
+                    const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 0 ? xa : 0.0, kq == 0 ? xb : 0.0, z, 0, 0, 0);
+                    const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 1 ? xa : 0.0, kq == 1 ? xb : 0.0, z, 0, 0, 0);
+                    const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 2 ? xa : 0.0, kq == 2 ? xb : 0.0, z, 0, 0, 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = 16 * I + (lane >> 4) + 4 * r;
+                        if (row < n && cb < row) {
+                            const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
+                            const double d2 = (sq[row] + sq[cb]) - 2.0 * dot;
+                            L[c2(row) + cb] = (float)sqrt(fmax(d2, 0.0));
+                        }
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            continue;
+        }
         // lane p holds cloud row p; all loads issued together
         const int pl = lane < n ? lane : n - 1;
         double px[3];
@@ -1150,7 +1189,7 @@ hipError_t launch_betti_dist(hipStream_t st, const BettiLaunch& b, const DistLau
 }
 
 // ---------------------------------------------------------------------------------------
-int betti_max_points() { return 64; }
+int betti_max_points() { return kWideMaxPoints; }
 int64_t betti_scratch_bytes_per_wave() { return ScratchLayout::total; }
 
 static int np_for(int max_points) { return max_points <= 32 ? 32 : (max_points <= 48 ? 48 : 64); }
@@ -1165,20 +1204,28 @@ int betti_grid_waves(int device) {
     return prop.multiProcessorCount * per_cu;
 }
 
-// route complexes with more than np_small points to the overflow list (wave-aggregated append)
+// route complexes above np_small points: up to 64 to the overflow list (NP = 64 launch), above
+// 64 to the wide list (betti_wide_kernel); wave-aggregated appends
 __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small) {
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int n = 0;
-    if (gi < bl.num_atoms)
-        n = bl.npoints[gi];
-    const bool big = gi < bl.num_atoms && n > np_small;
-    const uint64_t bal = ballot(big);
-    if (!bal) return;
-    const int leader = __ffsll((unsigned long long)bal) - 1;
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(bl.overflow_len, (uint32_t)__popcll(bal));
-    base = (uint32_t)__shfl((int)base, leader, kWave);
-    if (big) bl.overflow_list[base + mask_prefix(bal)] = (int32_t)gi;
+    const int n = gi < bl.num_atoms ? bl.npoints[gi] : 0;
+    const bool mid = gi < bl.num_atoms && n > np_small && n <= 64;
+    const bool wide = gi < bl.num_atoms && n > 64;
+    const uint64_t bm = ballot(mid), bw = ballot(wide);
+    if (bm) {
+        const int leader = __ffsll((unsigned long long)bm) - 1;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(bl.overflow_len, (uint32_t)__popcll(bm));
+        base = (uint32_t)__shfl((int)base, leader, kWave);
+        if (mid) bl.overflow_list[base + mask_prefix(bm)] = (int32_t)gi;
+    }
+    if (bw) {
+        const int leader = __ffsll((unsigned long long)bw) - 1;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(bl.wide_len, (uint32_t)__popcll(bw));
+        base = (uint32_t)__shfl((int)base, leader, kWave);
+        if (wide) bl.wide_list[base + mask_prefix(bw)] = (int32_t)gi;
+    }
 }
 
 template <int NP>
@@ -1204,17 +1251,19 @@ static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int g
     return launch_np<64>(st, b, grid_waves, max_items);
 }
 
-// Two-level dispatch: the main launch uses the instantiation sized for typical complexes
+// Three-level dispatch: the main launch uses the instantiation sized for typical complexes
 // (NP <= 48: about half the LDS of NP = 64, so twice the resident waves); complexes above it
-// are listed by betti_bucket_kernel and reduced by an NP = 64 launch. Counters and the list
-// length live on the device, so nothing synchronizes with the host in between.
-hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves) {
-    const int np_big = np_for(max_points);
+// are listed by betti_bucket_kernel and reduced by an NP = 64 launch (49..64 points) and by
+// betti_wide_kernel (65..512 points). Counters and list lengths live on the device, so nothing
+// synchronizes with the host in between.
+hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
+                        int wide_waves) {
+    const int np_big = np_for(max_points < 64 ? max_points : 64);
     const int np_main = np_big > 48 ? 48 : np_big;
     BettiLaunch m = b;
     m.work_list = nullptr;
     m.queue = b.work_counter;
-    m.skip_above = np_big > np_main ? 1 : 0;
+    m.skip_above = max_points > np_main ? 1 : 0;
     if (m.skip_above) {
         const int64_t blocks = (b.num_atoms + 255) / 256;
         hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main);
@@ -1223,11 +1272,16 @@ hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, in
     }
     hipError_t e = launch_for(np_main, st, m, grid_waves, b.num_atoms);
     if (e != hipSuccess || !m.skip_above) return e;
-    BettiLaunch o = b;
-    o.work_list = b.overflow_list;
-    o.queue = b.work_counter2;
-    o.skip_above = 0;
-    return launch_for(np_big, st, o, grid_waves, b.num_atoms);
+    if (np_big > np_main) {
+        BettiLaunch o = b;
+        o.work_list = b.overflow_list;
+        o.queue = b.work_counter2;
+        o.skip_above = 0;
+        e = launch_for(np_big, st, o, grid_waves, b.num_atoms);
+        if (e != hipSuccess) return e;
+    }
+    if (max_points > 64 && wide) e = launch_betti_wide(st, b, *wide, wide_waves);
+    return e;
 }
 
 }  // namespace dgn

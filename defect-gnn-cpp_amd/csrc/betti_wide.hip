@@ -1,0 +1,841 @@
+// betti_wide.hip — Vietoris–Rips persistence (dim 0/1/2, Z/2) and the 35 Betti statistics for
+// local complexes of 65..512 points, one wave64 per complex, for gfx950.
+//
+// The reference's default cutoff is 10 A (compute_structure_betti_features,
+// include/topology/betti_features.hpp:37-39; preprocess_betti.cpp:32,117): FCC-256 complexes
+// then have ~340 points. betti_kernels.hip covers n <= 64 with
+// one lane per vertex and the complex in LDS; this kernel runs the same algorithm with the
+// same output contract on larger complexes:
+//   * vertex sets are multi-word bitsets in LDS (kWW 64-bit words per vertex); lane k handles
+//     vertices k, k + 64, ...;
+//   * the f32 distance matrix is stored full and row-major in per-wave scratch, so the
+//     lane-per-vertex reads of one row are coalesced;
+//   * simplices are named by their combinatorial index (Ripser's colex numbering,
+//     ripser.cpp:181-201): a key is (diameter bits << 32) | ~index, so ascending keys are
+//     Ripser's filtration order (greater_diameter_or_smaller_index, ripser.cpp:318-324);
+//     vertices travel packed 9 bits per vertex, descending;
+//   * the non-apparent columns are bitonic-sorted in scratch, the serially resolved pivots live
+//     in an open-addressing hash table in scratch, the min-cofacet tables hold u16 vertices.
+// Pairing semantics as betti_kernels.hip: dim 0 by Prim on F-keys (Kruskal's forest in Ripser's
+// order, ripser.cpp:725-762); dim 1/2 cohomology with clearing, apparent pairs settled
+// lane-parallel, the rest reduced in Ripser's column order (decreasing F-key); death > birth
+// only, essential dim >= 1 classes are not emitted (ripser.cpp:1209-1225, 1240). The pairing
+// of a total order is unique, so the emitted multiset equals Ripser's.
+#include "dgn_internal.hpp"
+
+namespace dgn {
+namespace {
+
+constexpr int kWW = kWideMaxPoints / 64;  // bitset words per vertex
+constexpr uint64_t kInfW = ~0ull;
+constexpr uint32_t kNoneW = 0xFFFFFFFFu;
+constexpr uint16_t kMcNoneW = 0xFFFF;     // not a column, or no cofacet
+constexpr uint16_t kMcClearedW = 0xFFFE;  // triangle is the pivot of a dim-1 column (clearing)
+constexpr uint32_t kLazyW = 0x80000000u;  // pivot meta: V = {column simplex} (packed, low bits)
+// error bits (decoded in dgn_api.cpp)
+constexpr uint32_t kEPoints = 1u << 0, kEWork = 1u << 1, kENA = 1u << 2, kEPiv = 1u << 3, kEPairs = 1u << 4,
+                   kER = 1u << 5, kEGuard = 1u << 7;
+
+__device__ __forceinline__ uint64_t bin2(uint64_t v) { return v * (v - 1) / 2; }
+__device__ __forceinline__ uint64_t bin3(uint64_t v) { return v * (v - 1) * (v - 2) / 6; }
+__device__ __forceinline__ uint64_t bin4(uint64_t v) { return v * (v - 1) * (v - 2) * (v - 3) / 24; }
+__device__ __forceinline__ uint64_t wkey(uint32_t dbits, uint64_t idx) {
+    return ((uint64_t)dbits << 32) | (uint64_t)(~(uint32_t)idx);
+}
+__device__ __forceinline__ uint32_t rlw(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+__device__ __forceinline__ uint64_t rlw64(uint64_t x, int l) {
+    return ((uint64_t)rlw((uint32_t)(x >> 32), l) << 32) | rlw((uint32_t)x, l);
+}
+__device__ __forceinline__ uint32_t uniw(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uniw64(uint64_t x) {
+    return ((uint64_t)uniw((uint32_t)(x >> 32)) << 32) | uniw((uint32_t)x);
+}
+__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// packed simplex: vertices 9 bits each, descending, the smallest in the low field
+__device__ __forceinline__ int pv(uint64_t p, int field) { return (int)((p >> (9 * field)) & 511); }
+// combinatorial index of a packed simplex with nv vertices
+__device__ __forceinline__ uint64_t pidx(int nv, uint64_t p) {
+    if (nv == 2) return bin2(pv(p, 1)) + pv(p, 0);
+    if (nv == 3) return bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
+    return bin4(pv(p, 3)) + bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
+}
+// insert vertex x (not in p) into a packed simplex of nv vertices
+__device__ __forceinline__ uint64_t pinsert(int nv, uint64_t p, int x) {
+    int below = 0;
+    for (int t = 0; t < nv; ++t) below += pv(p, t) < x;
+    const uint64_t mask = (1ull << (9 * below)) - 1;
+    return ((p & ~mask) << 9) | ((uint64_t)x << (9 * below)) | (p & mask);
+}
+__device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
+
+struct WideCx {
+    const BettiLaunch& bl;
+    const WideLayout& ly;
+    uint64_t* adj;  // LDS [kWideMaxPoints][kWW]
+    uint16_t* par;  // LDS [kWideMaxPoints]: spanning-forest parent, 0xFFFF = root
+    uint8_t* scr;
+    int n, W;
+    float thr;
+    uint32_t err;
+    int n_d0, n_inf0, n_p1, n_p2;
+
+    template <class T>
+    __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
+    __device__ uint32_t d(int i, int j) const { return sp<uint32_t>(ly.D)[(int64_t)i * n + j]; }
+    __device__ uint64_t aw(int v, int w) const { return adj[v * kWW + w]; }
+    __device__ bool is_tree(int i, int j) const { return par[i] == j || par[j] == i; }
+    __device__ uint32_t sdiam(int dim, uint64_t p) const {  // dim 1: edge, dim 2: triangle
+        if (dim == 1) return d(pv(p, 1), pv(p, 0));
+        return max(max(d(pv(p, 2), pv(p, 1)), d(pv(p, 2), pv(p, 0))), d(pv(p, 1), pv(p, 0)));
+    }
+
+    // ---- distance matrix (mirrored from the packed lower triangle) + adjacency bitsets ----
+    __device__ void load(int64_t gi) {
+        const int lane = lane_id();
+        const float* L = bl.lower + gi * bl.tri_stride;
+        float* D = sp<float>(ly.D);
+        for (int i = lane; i < n * kWW; i += kWave) adj[i] = 0ull;
+        for (int i = lane; i < n; i += kWave) D[(int64_t)i * n + i] = 0.0f;
+        wave_lds_order();
+        for (int i = 1; i < n; ++i) {
+            for (int j0 = 0; j0 < i; j0 += kWave) {
+                const int j = j0 + lane;
+                bool e = false;
+                if (j < i) {
+                    const float v = L[c2i(i) + j];
+                    D[(int64_t)i * n + j] = v;
+                    D[(int64_t)j * n + i] = v;
+                    e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
+                }
+                const uint64_t b = ballot(e);
+                if (lane == 0) adj[i * kWW + (j0 >> 6)] = b;  // row i, columns j < i
+                if (e) atomicOr((unsigned long long*)&adj[j * kWW + (i >> 6)], 1ull << (i & 63));
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- dim 0: Prim on F-keys == Kruskal's forest in Ripser's order (ripser.cpp:725-762) ----
+    __device__ void prim() {
+        const int lane = lane_id();
+        float* d0s = sp<float>(ly.d0);
+        uint64_t best[kWW];
+        int bp[kWW];
+        uint32_t intree = lane == 0 ? 1u : 0u;  // bit t: vertex 64 t + lane is in the forest
+        for (int i = lane; i < n; i += kWave) par[i] = 0xFFFF;
+#pragma unroll
+        for (int t = 0; t < kWW; ++t) {
+            const int v = 64 * t + lane;
+            best[t] = kInfW;
+            bp[t] = 0;
+            if (t < W && v < n && v != 0 && ((aw(0, t) >> lane) & 1ull)) best[t] = wkey(d(0, v), bin2(v));
+        }
+        wave_lds_order();
+        n_inf0 = 1;
+        n_d0 = 0;
+        for (int added = 1; added < n; ++added) {
+            uint64_t lmin = kInfW;
+            int lt = 0, lp = 0, lfree = 1 << 30;
+#pragma unroll
+            for (int t = 0; t < kWW; ++t) {
+                const int v = 64 * t + lane;
+                const bool out = t < W && v < n && !((intree >> t) & 1u);
+                if (out && best[t] < lmin) {
+                    lmin = best[t];
+                    lt = t;
+                    lp = bp[t];
+                }
+                if (out && v < lfree) lfree = v;
+            }
+            const uint64_t m = wave_min(lmin);
+            int v;
+            if (m == kInfW) {  // new component: lowest vertex outside the forest
+                v = wave_min(lfree);
+                ++n_inf0;
+            } else {
+                const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
+                v = 64 * (int)rlw((uint32_t)lt, l) + l;
+                const int u = (int)rlw((uint32_t)lp, l);
+                const uint32_t dd = (uint32_t)(m >> 32);
+                if (dd != 0u) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
+                    if (lane == 0) d0s[n_d0] = __uint_as_float(dd);
+                    ++n_d0;
+                }
+                if (lane == 0) par[v] = (uint16_t)u;
+            }
+            if (lane == (v & 63)) intree |= 1u << (v >> 6);
+            wave_lds_order();
+#pragma unroll
+            for (int t = 0; t < kWW; ++t) {
+                const int w = 64 * t + lane;
+                if (t < W && w < n && !((intree >> t) & 1u) && ((aw(v, t) >> lane) & 1ull)) {
+                    const uint64_t k = wkey(d(v, w), v > w ? bin2(v) + w : bin2(w) + v);
+                    if (k < best[t]) {
+                        best[t] = k;
+                        bp[t] = v;
+                    }
+                }
+            }
+        }
+        wave_lds_order();
+    }
+
+    // ---- edges (i > j, d <= thr) in index order ----
+    __device__ int edge_list() {
+        const int lane = lane_id();
+        uint32_t* edges = sp<uint32_t>(ly.edges);
+        int off = 0;
+        for (int i = 1; i < n; ++i)
+            for (int w = 0; 64 * w < i; ++w) {
+                uint64_t bits = aw(i, w);
+                const int lim = i - 64 * w;
+                if (lim < 64) bits &= (1ull << lim) - 1ull;
+                if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = ((uint32_t)i << 9) | (uint32_t)(64 * w + lane);
+                off += __popcll(bits);
+            }
+        __syncthreads();
+        return off;
+    }
+
+    // F-minimal cofacet of sigma (dim 1: edge a > b; dim 2: triangle a > b > c, packed sp_) over
+    // the common-neighbour bitset cand: its key (kInf if none), packed vertices and added vertex.
+    // Walking k downwards, the first k with all distances <= diam is the F-minimal cofacet
+    // (largest index at the smallest diameter) and ends the walk (found); its distances to
+    // a, b, c are returned for the apparent test.
+    __device__ uint64_t min_cofacet(int dim, int a, int b, int c, uint32_t dsig, uint64_t sp_, const uint64_t* cand,
+                                    uint64_t& bestp, int& bk, bool& found, uint32_t& hda, uint32_t& hdb,
+                                    uint32_t& hdc) const {
+        uint64_t best = kInfW;
+        found = false;
+        bk = 0;
+        bestp = 0;
+#pragma unroll
+        for (int w = kWW - 1; w >= 0; --w) {
+            if (w >= W || found) continue;
+            uint64_t m = cand[w];
+            while (m) {
+                const int bit = 63 - __clzll((long long)m);
+                m &= ~(1ull << bit);
+                const int k = 64 * w + bit;
+                const uint32_t da = d(a, k), db_ = d(b, k), dc = dim == 2 ? d(c, k) : 0u;
+                const uint32_t dk = max(max(da, db_), dc);
+                const uint64_t p = pinsert(dim + 1, sp_, k);
+                const uint64_t idx = pidx(dim + 2, p);
+                if (dk <= dsig) {
+                    best = wkey(dsig, idx);
+                    bestp = p;
+                    bk = k;
+                    found = true;
+                    hda = da;
+                    hdb = db_;
+                    hdc = dc;
+                    break;
+                }
+                const uint64_t kk = wkey(dk, idx);
+                if (kk < best) {
+                    best = kk;
+                    bestp = p;
+                    bk = k;
+                }
+            }
+        }
+        return best;
+    }
+
+    // append a non-apparent column (lanes with `na`) to the scratch list
+    __device__ void na_append(bool na, int& nna, uint64_t colkey, uint64_t tau, uint64_t tv, uint32_t colp) {
+        const uint64_t bal = ballot(na);
+        if (na) {
+            const int slot = nna + mask_prefix(bal);
+            if (slot < ly.na_cap) {
+                sp<uint64_t>(ly.na_key)[slot] = colkey;
+                sp<uint64_t>(ly.na_tau)[slot] = tau;
+                sp<uint64_t>(ly.na_tv)[slot] = tv;
+                sp<uint32_t>(ly.na_col)[slot] = colp;
+            }
+        }
+        nna += __popcll(bal);
+    }
+
+    // ---- dim 1: one lane per column (non-tree edge) ----
+    __device__ int pass_dim1(int n_edges) {
+        const int lane = lane_id();
+        const uint32_t* edges = sp<uint32_t>(ly.edges);
+        uint16_t* mc_e = sp<uint16_t>(ly.mc_e);
+        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+        int nna = 0;
+        for (int base = 0; base < n_edges; base += kWave) {
+            const int e = base + lane;
+            bool na = false;
+            uint64_t colkey = 0, best = kInfW, bestp = 0;
+            uint32_t colp = 0;
+            if (e < n_edges) {
+                const uint32_t ed = edges[e];
+                const int i = (int)(ed >> 9), j = (int)(ed & 511);
+                uint16_t mc = kMcNoneW;
+                if (!is_tree(i, j)) {
+                    const uint32_t dij = d(i, j);
+                    colp = ed;
+                    colkey = wkey(dij, bin2(i) + j);
+                    uint64_t cand[kWW];
+#pragma unroll
+                    for (int w = 0; w < kWW; ++w) cand[w] = w < W ? (aw(i, w) & aw(j, w)) : 0ull;
+                    bool found;
+                    int bk;
+                    uint32_t hda = 0, hdb = 0, hdc = 0;
+                    best = min_cofacet(1, i, j, 0, dij, ed, cand, bestp, bk, found, hda, hdb, hdc);
+                    if (best != kInfW) {
+                        // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet:
+                        // the facets with k replacing a larger vertex must be strictly shorter
+                        const bool app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
+                        if (app) mc_t[pidx(3, bestp)] = kMcClearedW;  // clearing for dim 2
+                        else na = true;
+                        mc = (uint16_t)bk;
+                    }
+                }
+                mc_e[bin2(i) + j] = mc;
+            }
+            // apparent pairs have zero persistence: nothing to emit
+            na_append(na, nna, colkey, best, bestp, colp);
+        }
+        __syncthreads();
+        return nna;
+    }
+
+    // ---- dim 2: one lane per column (uncleared triangle), triangles streamed edge by edge ----
+    __device__ int pass_dim2(int n_edges) {
+        const uint32_t* edges = sp<uint32_t>(ly.edges);
+        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+        int nna = 0, next_edge = 0;
+        int ea = 0, eb = 0, tw = -1;  // current edge (a > b) and word of c < b
+        uint64_t tm = 0;              // remaining c of the current word
+        for (;;) {
+            for (;;) {
+                while (tm == 0ull && tw >= 0) {  // next word of the current edge
+                    ++tw;
+                    if (64 * tw >= eb) {
+                        tw = -1;
+                        break;
+                    }
+                    tm = aw(ea, tw) & aw(eb, tw);
+                    const int lim = eb - 64 * tw;
+                    if (lim < 64) tm &= (1ull << lim) - 1ull;
+                }
+                const bool need = tm == 0ull;
+                const uint64_t bal = ballot(need);
+                if (!bal || next_edge >= n_edges) break;
+                const int e = next_edge + mask_prefix(bal);
+                if (need && e < n_edges) {
+                    const uint32_t ed = edges[e];
+                    ea = (int)(ed >> 9);
+                    eb = (int)(ed & 511);
+                    tw = 0;
+                    tm = aw(ea, 0) & aw(eb, 0);
+                    if (eb < 64) tm &= (1ull << eb) - 1ull;
+                }
+                next_edge += __popcll(bal);
+            }
+            const bool active = tm != 0ull;
+            if (!ballot(active)) break;
+            bool na = false;
+            uint64_t colkey = 0, best = kInfW, bestp = 0;
+            uint32_t colp = 0;
+            if (active) {
+                const int a = ea, b = eb, c = 64 * tw + __ffsll((unsigned long long)tm) - 1;
+                tm &= tm - 1ull;
+                const uint64_t tidx = bin3(a) + bin2(b) + c;
+                uint16_t mc = kMcNoneW;
+                if (mc_t[tidx] != kMcClearedW) {
+                    const uint32_t dab = d(a, b), dac = d(a, c), dbc = d(b, c);
+                    const uint32_t ds = max(max(dab, dac), dbc);
+                    colp = ((uint32_t)a << 18) | ((uint32_t)b << 9) | (uint32_t)c;
+                    colkey = wkey(ds, tidx);
+                    uint64_t cand[kWW];
+#pragma unroll
+                    for (int w = 0; w < kWW; ++w) cand[w] = w < W ? (aw(a, w) & aw(b, w) & aw(c, w)) : 0ull;
+                    bool found;
+                    int bk;
+                    uint32_t hda = 0, hdb = 0, hdc = 0;
+                    best = min_cofacet(2, a, b, c, ds, colp, cand, bestp, bk, found, hda, hdb, hdc);
+                    if (best != kInfW) {
+                        const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
+                                         (bk > b || max(max(hda, hdc), dac) < ds) &&
+                                         (bk > c || max(max(hda, hdb), dab) < ds);
+                        na = !app;
+                        mc = (uint16_t)bk;
+                    }
+                }
+                mc_t[tidx] = mc;
+            }
+            na_append(na, nna, colkey, best, bestp, colp);
+        }
+        __syncthreads();
+        return nna;
+    }
+
+    // ---- non-apparent columns in Ripser's order: bitonic sort, key descending ----
+    __device__ void sort_na(int cnt) {
+        const int lane = lane_id();
+        int N = 1;
+        while (N < cnt) N <<= 1;
+        uint64_t* K = sp<uint64_t>(ly.na_key);
+        uint64_t* T = sp<uint64_t>(ly.na_tau);
+        uint64_t* V = sp<uint64_t>(ly.na_tv);
+        uint32_t* Cc = sp<uint32_t>(ly.na_col);
+        for (int i = cnt + lane; i < N; i += kWave) K[i] = 0ull;  // padding sorts last
+        __syncthreads();
+        for (int k = 2; k <= N; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = lane; i < N; i += kWave) {
+                    const int l = i ^ j;
+                    if (l > i) {
+                        const uint64_t x = K[i], y = K[l];
+                        if (((i & k) == 0) ? (x < y) : (x > y)) {
+                            K[i] = y;
+                            K[l] = x;
+                            const uint64_t t0 = T[i], v0 = V[i];
+                            const uint32_t c0 = Cc[i];
+                            T[i] = T[l];
+                            V[i] = V[l];
+                            Cc[i] = Cc[l];
+                            T[l] = t0;
+                            V[l] = v0;
+                            Cc[l] = c0;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+    }
+
+    // ---- serially resolved pivots: open-addressing hash table (key 0 = empty) ----
+    __device__ static uint32_t hmix(uint64_t k) {
+        k ^= k >> 33;
+        k *= 0xff51afd7ed558ccdull;
+        k ^= k >> 33;
+        return (uint32_t)k;
+    }
+    __device__ uint32_t hfind(uint64_t k) const {
+        const int lane = lane_id();
+        const uint64_t* HK = sp<uint64_t>(ly.h_key);
+        const uint32_t* HM = sp<uint32_t>(ly.h_meta);
+        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
+        const uint32_t base = hmix(k) & mask;
+        for (int probe = 0; probe < ly.h_cap; probe += kWave) {
+            const uint64_t x = HK[(base + (uint32_t)(probe + lane)) & mask];
+            const uint64_t hit = ballot(x == k), emp = ballot(x == 0ull);
+            const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
+            const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
+            if (fh < fe) return uniw(HM[(base + (uint32_t)(probe + fh)) & mask]);
+            if (fe < kWave) return kNoneW;
+        }
+        return kNoneW;
+    }
+    __device__ bool hinsert(uint64_t k, uint32_t meta, int npiv) {
+        const int lane = lane_id();
+        uint64_t* HK = sp<uint64_t>(ly.h_key);
+        uint32_t* HM = sp<uint32_t>(ly.h_meta);
+        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
+        const uint32_t base = hmix(k) & mask;
+        if (npiv >= ly.na_cap) return false;
+        for (int probe = 0; probe < ly.h_cap; probe += kWave) {
+            const uint64_t x = HK[(base + (uint32_t)(probe + lane)) & mask];
+            const uint64_t emp = ballot(x == 0ull);
+            if (emp) {
+                const uint32_t slot = (base + (uint32_t)(probe + __ffsll((unsigned long long)emp) - 1)) & mask;
+                if (lane == 0) {
+                    HK[slot] = k;
+                    HM[slot] = meta;
+                    sp<uint32_t>(ly.h_used)[npiv] = slot;
+                }
+                __syncthreads();  // the next lookups (other lanes) see it
+                return true;
+            }
+        }
+        return false;
+    }
+
+    // Apparent owner of the pivot tau (packed, dim + 2 vertices; whole wave, uniform): its F-max
+    // facet f if tau is f's F-minimal cofacet (recorded by the lane-parallel pass; tree edges and
+    // cleared triangles hold kMcNone), else kNone.
+    __device__ uint32_t apparent_owner(int dim, uint64_t tv) const {
+        const int nv = dim + 2;
+        int v[4];
+        for (int t = 0; t < nv; ++t) v[t] = pv(tv, nv - 1 - t);  // v[0] largest
+        uint32_t dd[4][4];
+        for (int s = 0; s < nv; ++s)
+            for (int t = s + 1; t < nv; ++t) dd[s][t] = uniw(d(v[s], v[t]));
+        uint64_t bestk = 0, bestf = 0;
+        int drop = 0;
+        for (int t = 0; t < nv; ++t) {  // facet without v[t]
+            uint32_t diam = 0;
+            uint64_t f = 0;
+            for (int s = 0; s < nv; ++s) {
+                if (s == t) continue;
+                f = (f << 9) | (uint64_t)v[s];
+                for (int u = s + 1; u < nv; ++u)
+                    if (u != t) diam = max(diam, dd[s][u]);
+            }
+            const uint64_t kk = wkey(diam, pidx(nv - 1, f));
+            if (kk > bestk) {
+                bestk = kk;
+                bestf = f;
+                drop = t;
+            }
+        }
+        const uint16_t m = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
+        return uniw(m) == (uint32_t)v[drop] ? (uint32_t)bestf : kNoneW;
+    }
+
+    // ---- the working column's V list (scratch: vlist[0..v), packed simplices, no small cap) ----
+    __device__ int v_find(uint32_t x, int v) const {
+        const int lane = lane_id();
+        const uint32_t* VL = sp<uint32_t>(ly.vlist);
+        for (int base = 0; base < v; base += kWave) {
+            const uint32_t y = base + lane < v ? VL[base + lane] : kNoneW;
+            const uint64_t bal = ballot(y == x);
+            if (bal) return base + __ffsll((unsigned long long)bal) - 1;
+        }
+        return -1;
+    }
+    __device__ bool v_toggle(uint32_t x, int& v) {  // V ^= {x}; false on overflow
+        uint32_t* VL = sp<uint32_t>(ly.vlist);
+        const int pos = v_find(x, v);
+        if (pos >= 0) {
+            if (pos != v - 1) {
+                const uint32_t last = uniw(VL[v - 1]);
+                if (lane_id() == 0) VL[pos] = last;
+            }
+            v = v - 1;
+        } else {
+            if (v >= ly.vl_cap) return false;
+            if (lane_id() == 0) VL[v] = x;
+            v = v + 1;
+        }
+        __syncthreads();  // the list (scratch) is read by every lane next
+        return true;
+    }
+
+    // Pivot of sum(delta s, s in V) above `floor` (the previous pivot): lane k evaluates the
+    // cofacets s u {x}, x = 64 t + k; a cofacet arises once per facet in V; the multiplicity of
+    // the minimum is summed over lanes (a lane can meet it from several words). Even: raise the
+    // floor and repeat. Returns kInf for the zero column; tv = packed pivot.
+    __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
+        const int k = lane_id();
+        const uint32_t* VL = sp<uint32_t>(ly.vlist);
+        uint32_t* VD = sp<uint32_t>(ly.vdiam);
+        for (int i = k; i < v; i += kWave) VD[i] = sdiam(dim, VL[i]);
+        __syncthreads();
+        for (;;) {
+            uint64_t lmin = kInfW, lp = 0;
+            int lcnt = 0;
+            for (int i = 0; i < v; ++i) {
+                const uint32_t s = uniw(VL[i]);
+                const uint32_t ds = uniw(VD[i]);
+                const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
+                const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
+                const int c = pv(s, 0);
+                for (int t = 0; t < W; ++t) {
+                    const int x = 64 * t + k;
+                    uint64_t am = aw(a, t) & aw(b, t);
+                    if (dim == 2) am &= aw(c, t);
+                    const bool on = x < n && ((am >> k) & 1ull);
+                    const int xc = x < n ? x : n - 1;
+                    uint32_t dd = max(ds, max(d(a, xc), d(b, xc)));
+                    if (dim == 2) dd = max(dd, d(c, xc));
+                    const uint64_t p = pinsert(dim + 1, s, xc);
+                    const uint64_t kk = wkey(dd, pidx(dim + 2, p));
+                    if (on && kk > floor) {
+                        if (kk < lmin) {
+                            lmin = kk;
+                            lcnt = 1;
+                            lp = p;
+                        } else if (kk == lmin) {
+                            ++lcnt;
+                        }
+                    }
+                }
+            }
+            const uint64_t m = wave_min(lmin);
+            if (m == kInfW) return kInfW;
+            const int cnt = wave_sum(lmin == m ? lcnt : 0);
+            if (cnt & 1) {
+                const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
+                tv = rlw64(lp, l);
+                return m;
+            }
+            floor = m;
+        }
+    }
+
+    // ---- the non-apparent columns of one dimension, in Ripser's order ----
+    __device__ void reduce(int dim, int nna) {
+        const int lane = lane_id();
+        if (nna > ly.na_cap) {
+            err |= kENA;
+            return;
+        }
+        sort_na(nna);
+        const uint64_t* K = sp<uint64_t>(ly.na_key);
+        const uint64_t* T = sp<uint64_t>(ly.na_tau);
+        const uint64_t* V = sp<uint64_t>(ly.na_tv);
+        const uint32_t* Cc = sp<uint32_t>(ly.na_col);
+        uint32_t* vstore = sp<uint32_t>(ly.vstore);
+        float2* pairs = sp<float2>(dim == 1 ? ly.p1 : ly.p2);
+        int& np = dim == 1 ? n_p1 : n_p2;
+        int npiv = 0, vused = 0;
+        for (int ci = 0; ci < nna && err == 0u; ++ci) {
+            const uint64_t colkey = uniw64(K[ci]);
+            uint64_t tau = uniw64(T[ci]);
+            uint64_t tv = uniw64(V[ci]);
+            const uint32_t cp = uniw(Cc[ci]);
+            const uint32_t birth = (uint32_t)(colkey >> 32);
+            uint32_t meta = hfind(tau);
+            uint32_t app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+            int v = 0;  // 0 = lazy: V == {this column}
+            if (meta != kNoneW || app != kNoneW) {
+                v_toggle(cp, v);
+                long guard = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (app != kNoneW) {
+                        ok = v_toggle(app, v);
+                    } else if (meta & kLazyW) {
+                        ok = v_toggle(meta & ~kLazyW, v);
+                    } else {
+                        const int off = (int)(meta >> 10), len = (int)(meta & 1023u);
+                        for (int t0 = 0; t0 < len && ok; t0 += kWave) {
+                            const uint32_t w = t0 + lane < len ? vstore[off + t0 + lane] : 0u;
+                            const int cnt = len - t0 < kWave ? len - t0 : kWave;
+                            for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(rlw(w, u), v);
+                        }
+                    }
+                    if (!ok) {
+                        err |= kEWork;
+                        break;
+                    }
+                    tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInfW;
+                    if (tau == kInfW) break;  // zero column: essential class, not emitted
+                    meta = hfind(tau);
+                    app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+                    if (meta == kNoneW && app == kNoneW) break;  // tau is this column's pivot
+                    if (++guard > (1l << 20)) {
+                        err |= kEGuard;
+                        break;
+                    }
+                }
+                if (err || tau == kInfW) continue;
+            }
+            const uint32_t death = (uint32_t)(tau >> 32);
+            if (__uint_as_float(death) > __uint_as_float(birth)) {
+                if (lane == 0 && np < ly.p_cap) pairs[np] = make_float2(__uint_as_float(birth), __uint_as_float(death));
+                ++np;
+            }
+            if (dim == 1 && lane == 0) sp<uint16_t>(ly.mc_t)[pidx(3, tv)] = kMcClearedW;  // clearing
+            uint32_t m;
+            if (v == 0) {
+                m = kLazyW | cp;
+            } else {
+                if (vused + v > ly.vs_cap || v > 1023) {
+                    err |= kER;
+                    break;
+                }
+                const uint32_t* VL = sp<uint32_t>(ly.vlist);
+                for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
+                __syncthreads();
+                m = ((uint32_t)vused << 10) | (uint32_t)v;
+                vused += v;
+            }
+            if (!hinsert(tau, m, npiv)) {
+                err |= kEPiv;
+                break;
+            }
+            ++npiv;
+        }
+        __syncthreads();
+        // empty the pivot table for the next dimension / complex
+        uint64_t* HK = sp<uint64_t>(ly.h_key);
+        const uint32_t* used = sp<uint32_t>(ly.h_used);
+        for (int i = lane; i < npiv; i += kWave) HK[used[i]] = 0ull;
+        __syncthreads();
+    }
+
+    // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) + outputs ----
+    __device__ void finish(int64_t gi, double weight) {
+        const int lane = lane_id();
+        double* feat = bl.features ? bl.features + 35 * gi : nullptr;
+        if (n_p1 > ly.p_cap || n_p2 > ly.p_cap) err |= kEPairs;
+        if (err) {
+            if (lane == 0) atomicOr(bl.error_flag, err);
+            if (feat && lane < 35) feat[lane] = __builtin_nan("");
+            if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
+            return;
+        }
+        const float* d0s = sp<float>(ly.d0);
+        const float2* P1 = sp<float2>(ly.p1);
+        const float2* P2 = sp<float2>(ly.p2);
+        double myval = 0.0;
+#pragma unroll 1
+        for (int g = 0; g < 7; ++g) {
+            const int m = g == 0 ? n_d0 : (g <= 3 ? n_p1 : n_p2);
+            double st[5] = {0, 0, 0, 0, 0};
+            if (m > 0) {
+                const float2* P = g <= 3 ? P1 : P2;
+                const int which = g == 0 ? 1 : ((g - 1) % 3 == 0 ? 2 : ((g - 1) % 3 == 1 ? 0 : 1));
+                double sum = 0.0, mx = -INFINITY, mn = INFINITY;
+                for (int i = lane; i < m; i += kWave) {
+                    double v;
+                    if (g == 0) {
+                        v = (double)d0s[i];
+                    } else {
+                        const float2 pr = P[i];
+                        v = which == 0 ? (double)pr.x : (which == 1 ? (double)pr.y : (double)pr.y - (double)pr.x);
+                    }
+                    sum += v;
+                    mx = fmax(mx, v);
+                    mn = fmin(mn, v);
+                }
+                sum = wave_sum(sum);
+                mx = wave_max(mx);
+                mn = wave_min(mn);
+                const double mean = sum / (double)m;
+                double ss = 0.0;
+                for (int i = lane; i < m; i += kWave) {
+                    double v;
+                    if (g == 0) {
+                        v = (double)d0s[i];
+                    } else {
+                        const float2 pr = P[i];
+                        v = which == 0 ? (double)pr.x : (which == 1 ? (double)pr.y : (double)pr.y - (double)pr.x);
+                    }
+                    ss += (v - mean) * (v - mean);
+                }
+                ss = wave_sum(ss);
+                st[0] = mean;
+                st[1] = sqrt(ss / (double)m);  // population std (math.hpp:13-16)
+                st[2] = mx;
+                st[3] = mn;
+                st[4] = sum * weight;  // weighted_sum = sum * weight (math.hpp:26-28)
+            }
+            const int r = lane - 5 * g;
+            if (r == 0) myval = st[0];
+            if (r == 1) myval = st[1];
+            if (r == 2) myval = st[2];
+            if (r == 3) myval = st[3];
+            if (r == 4) myval = st[4];
+        }
+        if (feat && lane < 35) feat[lane] = myval;
+        if (bl.pairs_out) {
+            float2* po = reinterpret_cast<float2*>(bl.pairs_out) + gi * 3 * bl.pair_cap;
+            for (int i = lane; i < n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, d0s[i]);
+            for (int i = lane; i < n_p1 && i < bl.pair_cap; i += kWave) po[bl.pair_cap + i] = P1[i];
+            for (int i = lane; i < n_p2 && i < bl.pair_cap; i += kWave) po[2 * bl.pair_cap + i] = P2[i];
+        }
+        if (bl.counts && lane == 0) {
+            bl.counts[4 * gi + 0] = n_d0;
+            bl.counts[4 * gi + 1] = n_inf0;
+            bl.counts[4 * gi + 2] = n_p1;
+            bl.counts[4 * gi + 3] = n_p2;
+        }
+    }
+
+    __device__ void run(int64_t gi, double weight) {
+        load(gi);
+        prim();
+        const int n_edges = edge_list();
+        const int nna1 = pass_dim1(n_edges);
+        reduce(1, nna1);
+        __syncthreads();  // clearing marks complete before the dim-2 pass reads them
+        if (err == 0u) {
+            const int nna2 = pass_dim2(n_edges);
+            reduce(2, nna2);
+        } else {
+            // no dim-2 pass consumes the clearing marks: erase every triangle entry
+            uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+            const int64_t nt = (int64_t)bin3((uint64_t)n);
+            for (int64_t t = lane_id(); t < nt; t += kWave) mc_t[t] = kMcNoneW;
+        }
+        __syncthreads();
+        finish(gi, weight);
+        __syncthreads();
+    }
+};
+
+__global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
+    __shared__ uint64_t adj[kWideMaxPoints * kWW];
+    __shared__ uint16_t par[kWideMaxPoints];
+    __shared__ int64_t q_s;
+    const int lane = lane_id();
+    uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
+    const int64_t total = (int64_t)*bl.wide_len;
+    for (;;) {
+        if (lane == 0) q_s = (int64_t)atomicAdd(bl.wide_queue, 1u);
+        __syncthreads();
+        const int64_t wi = q_s;
+        __syncthreads();
+        if (wi >= total) break;
+        const int64_t gi = (int64_t)bl.wide_list[wi];
+        const int n = bl.npoints[gi];
+        if (n > ly.nmax) {
+            if (lane == 0) atomicOr(bl.error_flag, kEPoints);
+            if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
+            if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
+            continue;
+        }
+        WideCx cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+        cx.run(gi, bl.weight ? bl.weight[gi] : 1.0);
+    }
+}
+
+int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+}  // namespace
+
+// Scratch layout of one wave for complexes of up to nmax points (all offsets 256-B aligned).
+WideLayout betti_wide_layout(int nmax) {
+    WideLayout l{};
+    const int64_t n = nmax;
+    const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
+    int64_t cap = 1024;
+    while (cap < t && cap < (int64_t(1) << 17)) cap <<= 1;
+    l.nmax = nmax;
+    l.na_cap = (int32_t)cap;
+    l.p_cap = (int32_t)cap;
+    l.h_cap = (int32_t)(2 * cap);
+    l.vs_cap = 1 << 20;
+    l.vl_cap = 1 << 16;
+    int64_t o = 0;
+    auto take = [&](int64_t bytes) {
+        const int64_t at = o;
+        o = align256(o + bytes);
+        return at;
+    };
+    l.D = take(4 * n * n);
+    l.mc_e = take(2 * e);
+    l.mc_t = take(2 * t);
+    l.edges = take(4 * e);
+    l.na_key = take(8 * cap);
+    l.na_tau = take(8 * cap);
+    l.na_tv = take(8 * cap);
+    l.na_col = take(4 * cap);
+    l.vstore = take(4 * (int64_t)l.vs_cap);
+    l.vlist = take(4 * (int64_t)l.vl_cap);
+    l.vdiam = take(4 * (int64_t)l.vl_cap);
+    l.h_key = take(8 * 2 * cap);
+    l.h_meta = take(4 * 2 * cap);
+    l.h_used = take(4 * cap);
+    l.p1 = take(8 * cap);
+    l.p2 = take(8 * cap);
+    l.d0 = take(4 * n);
+    l.total = o;
+    return l;
+}
+
+hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
+    if (waves <= 0) return hipSuccess;
+    hipLaunchKernelGGL(betti_wide_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, b, l);
+    return hipGetLastError();
+}
+
+}  // namespace dgn

@@ -63,7 +63,9 @@ struct Scalars {  // device-side scalars, one allocation
     uint32_t work_counter;   // betti main launch queue
     uint32_t work_counter2;  // betti overflow launch queue
     uint32_t overflow_len;   // complexes routed to the overflow launch
-    uint32_t pad[3];
+    uint32_t wide_queue;     // betti wide launch queue
+    uint32_t wide_len;       // complexes routed to the wide launch
+    uint32_t pad[1];
 };
 
 }  // namespace
@@ -87,7 +89,7 @@ struct dgn_ctx {
     int64_t cnt_edges = 0;
     double cnt_sum_sq = 0;
     // betti workspace
-    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w;
+    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
     int betti_slots = 0;
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
@@ -321,6 +323,22 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 4 * sizeof(uint32_t), c->stream));
     HIP_TRY(c, c->b_list.ensure(sizeof(int32_t) * (size_t)A));
+    // complexes above 64 points: the wide kernel, one wave per complex with a per-wave scratch
+    // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
+    WideLayout wl{};
+    int wide_waves = 0;
+    if (max_points > 64) {
+        wl = betti_wide_layout(max_points);
+        const int64_t budget = int64_t(8) << 30;
+        wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, 512, A}));
+        const size_t want = (size_t)wl.total * (size_t)wide_waves;
+        if (c->b_wide.bytes < want) {
+            HIP_TRY(c, c->b_wide.ensure(want));
+            HIP_TRY(c, hipMemsetAsync(c->b_wide.p, 0, c->b_wide.bytes, c->stream));  // empty pivot tables
+        }
+        wl.base = c->b_wide.as<uint8_t>();
+        HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
+    }
     BettiLaunch bl{};
     bl.row_ptr = given ? nullptr : c->b_row_ptr.as<int64_t>();
     bl.disp = given ? nullptr : c->b_disp.as<double>();
@@ -344,6 +362,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.cloud_stride = cloud_stride;
     bl.pairs_out = pairs_out;
     bl.pair_cap = pair_cap;
+    bl.wide_list = max_points > 64 ? c->b_wlist.as<int32_t>() : nullptr;
+    bl.wide_len = &sc->wide_len;
+    bl.wide_queue = &sc->wide_queue;
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, c->phase.ensure(32 * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
@@ -361,9 +382,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.features = features ? features + 35 * c0 : nullptr;
         pb.counts = counts ? counts + 4 * c0 : nullptr;
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
-        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 3 * sizeof(uint32_t), c->stream));
+        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 5 * sizeof(uint32_t), c->stream));
         TimedLaunch t(c, "betti_vr", bytes, 0.0);
-        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots));
+        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr, wide_waves));
         return DGN_OK;
     };
     if (lower) {
@@ -488,7 +509,8 @@ void dgn_ctx_destroy(dgn_ctx* c) {
     fold_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
     for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->block_aux, &c->atom_struct, &c->rows_d, &c->rows_j, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
-                      &c->b_disp, &c->b_scratch, &c->b_list, &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
+                      &c->b_disp, &c->b_scratch, &c->b_list, &c->b_lower, &c->b_np, &c->b_w, &c->b_wlist, &c->b_wide,
+                      &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
         b->release();
     if (c->host_scalars) (void)hipHostFree(c->host_scalars);
     if (c->own) (void)hipStreamDestroy(c->own);

@@ -91,11 +91,26 @@ struct BettiLaunch {
     float* pairs_out;
     int32_t pair_cap;
     unsigned long long* phase_cycles;  // [32] diagnostics build only (DGN_PHASE_TIMING)
+    // complexes above 64 points, listed by the bucket pass for betti_wide_kernel
+    int32_t* wide_list;       // [num_atoms]
+    uint32_t* wide_len;
+    uint32_t* wide_queue;
     // set by launch_betti per launch
     const int32_t* work_list; // null = all complexes 0..num_atoms-1
     uint32_t* queue;          // work counter of this launch
     int32_t skip_above;       // 1 = complexes above NP are left to the overflow launch
 };
+// wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout
+constexpr int kWideMaxPoints = 512;
+struct WideLayout {
+    uint8_t* base;  // scratch of wave w at base + w * total
+    int64_t total;
+    int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
+    int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2, d0;
+};
+WideLayout betti_wide_layout(int nmax);
+hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
+
 // distance pass over complexes [first, first + count) of a BettiLaunch's CSR / cloud input
 struct DistLaunch {
     int64_t first, count;
@@ -107,6 +122,8 @@ hipError_t launch_betti_dist(hipStream_t s, const BettiLaunch& b, const DistLaun
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();
 int betti_grid_waves(int device);
-hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int grid_waves);
+// main (<= 48 points) + overflow (49..64) + wide (65..512) launches; `wide` null if max_points <= 64
+hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
+                        int wide_waves);
 
 }  // namespace dgn

@@ -183,3 +183,38 @@ def structure_graph(lattice, pos, r_cutoff, max_neighbors, rbf_cutoff, dr, want_
     lib().oracle_structure_graph(_p(L, C.c_double), _p(P, C.c_double), P.shape[0], r_cutoff, k, 1e-10, rbf_cutoff,
                                  dr, _p(out, C.c_double))
     return out
+
+
+def statistics(pairs, which, weight):
+    """compute_statistics over one diagram (betti_features.cpp:24-55): which 0 birth, 1 death,
+    2 persistence; pairs [m][2] f32 sorted."""
+    P = np.ascontiguousarray(pairs, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros(5)
+    lib().oracle_statistics(_p(P, C.c_float), P.shape[0], which, weight, _p(out, C.c_double))
+    return out
+
+
+def atom_betti_from_pairs(r, weight):
+    """The 35 features of one atom from its persistence dict (betti_features.cpp:87-98)."""
+    f = [statistics(r["dim0"], 1, weight)]
+    for d in ("dim1", "dim2"):
+        f += [statistics(r[d], 2, weight), statistics(r[d], 0, weight), statistics(r[d], 1, weight)]
+    return np.concatenate(f)
+
+
+def ref_atom_betti(lattice, pos, species, r_cutoff, atoms, ripser=True):
+    """Features + counts of selected atoms (compute_atom_betti_features, betti_features.cpp:57-101)
+    with the verbatim vendored Ripser (or the restatement): for spot checks at large cutoffs."""
+    nl = neighbor_list(lattice, pos, r_cutoff, None)
+    rp = nl["row_ptr"]
+    feats, counts = [], []
+    for i in atoms:
+        cloud = np.vstack([pos[i], pos[i] + nl["disp"][rp[i]:rp[i + 1]]])
+        n = cloud.shape[0]
+        low = local_distances(cloud)
+        thr = np.float32(r_cutoff)
+        r = ref_persistence(low, n, thr) if ripser else persistence(low, n, thr)
+        w = 1.0 / float(np.sum(np.asarray(species) == species[i]))
+        feats.append(atom_betti_from_pairs(r, w))
+        counts.append([len(r["dim0"]), r["n_inf0"], len(r["dim1"]), len(r["dim2"])])
+    return np.array(feats), np.array(counts, np.int32)

@@ -1,0 +1,68 @@
+"""Wide local complexes (65..512 points: the reference's default 10 A cutoff) through the C ABI
+vs the reference's verbatim vendored Ripser (oracle/_ref) — counts and pairs bit-exact, the 35
+statistics within 1e-6 relative. Ripser takes ~1 s per 340-point complex on one core, so the
+10 A checks spot-check a few atoms."""
+import numpy as np
+import pytest
+
+import dgn
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+FEAT_RTOL, FEAT_ATOL = 1e-6, 1e-12
+
+
+def _ref(low, n, thr):
+    return O.ref_persistence(low, n, thr) if O.ref_available() else O.persistence(low, n, thr)
+
+
+def _check_clouds(ctx, clouds, npts, thr, cap):
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=cap)
+    bad = []
+    for c in range(len(npts)):
+        n = int(npts[c])
+        r = _ref(O.local_distances(clouds[c, :n]), n, np.float32(thr))
+        got = {"dim0": pairs[c, 0, :counts[c, 0]], "dim1": pairs[c, 1, :counts[c, 2]], "dim2": pairs[c, 2, :counts[c, 3]]}
+        ok = all(np.array_equal(np.array(sorted(map(tuple, got[d]))).reshape(-1, 2), r[d].reshape(-1, 2))
+                 for d in got) and counts[c, 1] == r["n_inf0"]
+        if not ok:
+            bad.append((c, n, counts[c].tolist(), [len(r[d]) for d in ("dim0", "dim1", "dim2")], r["n_inf0"]))
+    assert not bad, bad[:8]
+
+
+def test_wide_random_clouds(ctx):
+    rng = np.random.default_rng(21)
+    C, maxp = 24, 200
+    npts = rng.integers(65, maxp + 1, size=C).astype(np.int32)
+    clouds = np.zeros((C, maxp, 3))
+    for c in range(C):
+        if c % 4 == 0:
+            clouds[c, :npts[c]] = rng.integers(0, 6, size=(npts[c], 3))  # exact ties
+        else:
+            clouds[c, :npts[c]] = rng.uniform(0, 6, size=(npts[c], 3))
+    _check_clouds(ctx, clouds, npts, 2.0, 4096)
+
+
+def test_all_three_tiers_in_one_batch(ctx):
+    """2..150 points: <= 48 main launch, 49..64 overflow launch, 65.. wide kernel."""
+    rng = np.random.default_rng(23)
+    C, maxp = 60, 150
+    npts = rng.integers(2, maxp + 1, size=C).astype(np.int32)
+    npts[:4] = [40, 60, 100, 150]
+    clouds = np.zeros((C, maxp, 3))
+    for c in range(C):
+        clouds[c, :npts[c]] = rng.uniform(0, 5.5, size=(npts[c], 3))
+    _check_clouds(ctx, clouds, npts, 1.8, 4096)
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
+def test_fcc256_default_cutoff_10A(ctx):
+    """compute_structure_betti_features at the reference default r_cutoff = 10 (~340-point
+    complexes); spot-check atoms against the verbatim Ripser."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    f, c = ctx.host_betti(batch, 10.0)
+    assert not np.isnan(f).any()
+    atoms = [0, 77, 200]
+    fo, co = O.ref_atom_betti(batch["lattice"][0], batch["positions"], batch["species"], 10.0, atoms)
+    assert np.array_equal(c[atoms], co), (c[atoms], co)
+    np.testing.assert_allclose(f[atoms], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
