@@ -1,7 +1,8 @@
 // Persistence front end over the GPU VR reduction (dgn_host_persistence[_lower]); reference
 // src/topology/ripser_wrapper.cpp:11-70. Pairs are returned per dimension sorted by
 // (birth, death) — the multiset Ripser emits; dim0 ends with one (0, inf) per component
-// (ripser.cpp:759-761). Complexes above 64 points are rejected by the kernel (DGN_ERR_UNSUPPORTED).
+// (ripser.cpp:759-761). Complexes up to 512 points (64-point wave kernel + wide kernel); above that
+// the library returns DGN_ERR_UNSUPPORTED.
 #include <algorithm>
 #include <cmath>
 #include <limits>

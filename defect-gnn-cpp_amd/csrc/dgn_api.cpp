@@ -91,6 +91,7 @@ struct dgn_ctx {
     // betti workspace
     DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
     int betti_slots = 0;
+    int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's pivot tables were zeroed for
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
 #ifdef DGN_PHASE_TIMING
@@ -332,11 +333,17 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const int64_t budget = int64_t(8) << 30;
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, 512, A}));
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
-        if (c->b_wide.bytes < want) {
-            HIP_TRY(c, c->b_wide.ensure(want));
-            HIP_TRY(c, hipMemsetAsync(c->b_wide.p, 0, c->b_wide.bytes, c->stream));  // empty pivot tables
-        }
+        const bool grown = c->b_wide.bytes < want;
+        if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
+        if (grown || c->wide_nmax != max_points || c->wide_waves != wide_waves) {
+            // the layout depends on max_points: every wave's pivot hash table starts empty (key 0);
+            // afterwards each reduction empties the slots it used
+            HIP_TRY(c, hipMemset2DAsync(wl.base + wl.h_key, (size_t)wl.total, 0, 8 * (size_t)wl.h_cap,
+                                        (size_t)wide_waves, c->stream));
+            c->wide_nmax = max_points;
+            c->wide_waves = wide_waves;
+        }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
     BettiLaunch bl{};

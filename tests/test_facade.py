@@ -177,3 +177,22 @@ def test_preprocess_driver(tmp_path, golden):
             np.testing.assert_allclose(feat, golden[f"{sid}/betti5/features"], rtol=1e-6, atol=1e-12)
     raw = open(outdir / "pca_model.bin", "rb").read()
     assert np.frombuffer(raw[:4], np.int32)[0] == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "libdgn_ref.so")),
+                    reason="verbatim Ripser (oracle/_ref) not built")
+def test_preprocess_driver_default_cutoff(tmp_path, golden):
+    """preprocess_betti at the reference default r_cutoff = 10 (preprocess_betti.cpp:117):
+    ~300-point local complexes through the wide kernel; spot-check atoms of 741.vasp against
+    the verbatim Ripser (about 1 s per atom on one core)."""
+    import oracle_py as O
+    outdir = tmp_path / "processed10"
+    rc, _, err = _run([os.path.join(BIN, "preprocess_betti"), POSCARS, str(outdir), "10", "6", "4"])
+    assert rc == 0, err
+    raw = open(outdir / "betti" / "741.bin", "rb").read()
+    r, c = np.frombuffer(raw[:8], np.int32)
+    feat = np.frombuffer(raw[8:], np.float64).reshape(r, c, order="F")
+    atoms = [0, 57]
+    fo, _ = O.ref_atom_betti(golden["741/lattice"], golden["741/positions"], golden["741/species"], 10.0, atoms)
+    np.testing.assert_allclose(feat[atoms], fo, rtol=1e-6, atol=1e-12)
