@@ -400,9 +400,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         if (st) return st;
     } else {
         // distance pass (MFMA) + Betti pass per chunk of complexes; the triangle buffer is
-        // bounded (~4 GB) so arbitrarily large shards stream through it
+        // bounded (~16 GB of the 288 GB HBM) so arbitrarily large shards stream through it
         const int64_t tri_stride = std::max<int64_t>(1, (int64_t)max_points * (max_points - 1) / 2);
-        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(4) << 30) / (4 * tri_stride)));
+        const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(16) << 30) / (4 * tri_stride)));
         bl.tri_stride = tri_stride;  // the distance pass writes [chunk][tri_stride]
         HIP_TRY(c, c->b_lower.ensure(sizeof(float) * (size_t)(chunk * tri_stride)));
         HIP_TRY(c, c->b_np.ensure(sizeof(int32_t) * (size_t)chunk));
