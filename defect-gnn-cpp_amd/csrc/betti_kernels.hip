@@ -75,7 +75,8 @@ struct ScratchLayout {
     static constexpr int64_t mincof = vstore + 4 * kVStoreCap;       // uint8 [C(64,3)] triangles
     static constexpr int64_t mincof_e = mincof + (64 * 63 * 62 / 6);  // uint8 [C(64,2)] edges
     static constexpr int64_t edges = (mincof_e + (64 * 63 / 2) + 15) / 16 * 16;  // uint16 [C(64,2)] (i << 8 | j)
-    static constexpr int64_t total = edges + 2 * (64 * 63 / 2);
+    static constexpr int64_t tris = (edges + 2 * (64 * 63 / 2) + 15) / 16 * 16;  // uint32 [C(64,3)] packed triangles
+    static constexpr int64_t total = tris + 4 * (64 * 63 * 62 / 6);
 };
 
 template <int NP>
@@ -745,13 +746,30 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             {
                 // f32 strict lower triangle (ripser_wrapper.cpp:20-24 packing), mirrored into
                 // the full matrix; one coalesced read per row
+                // entry t of the packing is (i, j) with i = floor((1 + sqrt(1 + 8t)) / 2), j = t - c2(i);
+                // all loads of a lane are independent, four in flight per step
                 const float* L = bl.lower + gi * bl.tri_stride;
-                for (int i = 1; i < n; ++i)
-                    if (lane < i) {
-                        const float d = L[c2(i) + lane];
-                        s.D[i * S + lane] = d;
-                        s.D[lane * S + i] = d;
+                const int tot = c2(n);
+                for (int t0 = 0; t0 < tot; t0 += 4 * kWave) {
+                    float v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = t0 + u * kWave + lane;
+                        v[u] = t < tot ? L[t] : 0.0f;
                     }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int t = t0 + u * kWave + lane;
+                        int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
+                        i -= c2(i) > t;
+                        i += c2(i + 1) <= t;
+                        const int j = t - c2(i);
+                        if (t < tot) {
+                            s.D[i * S + j] = v[u];
+                            s.D[j * S + i] = v[u];
+                        }
+                    }
+                }
             }
             lds_sync();
             DGN_PHASE(0);
@@ -893,46 +911,73 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
             // ---- dim 2: one lane per column (uncleared triangle) ----
             if (dim_max >= 2 && cx.err == 0) {
                 int nna = 0;
-                // stream triangles: each lane owns an edge (a > b) and walks c < b in adj[a] & adj[b]
-                int next_edge = 0;
-                int ea = 0, eb = 0;
-                uint64_t tmask = 0;
-                while (true) {
-                    while (true) {  // refill lanes with empty masks
-                        const bool need = tmask == 0;
-                        const uint64_t bal = ballot(need);
-                        if (!bal || next_edge >= n_edges) break;
-                        const int e = next_edge + mask_prefix(bal);
-                        if (need && e < n_edges) {
-                            const uint32_t ed = edges[e];
-                            ea = ed >> 8;
-                            eb = ed & 255;
-                            tmask = s.adj[ea] & s.adj[eb] & ((1ull << eb) - 1ull);
+                // (2a) stream the complex's triangles into a scratch list: each lane owns an edge
+                // (a > b) and walks c < b in adj[a] & adj[b]; lanes refill from the edge list
+                uint32_t* tl = cx.template sp<uint32_t>(ScratchLayout::tris);
+                int ntri = 0;
+                {
+                    int next_edge = 0;
+                    int ea = 0, eb = 0;
+                    uint64_t tmask = 0;
+                    while (true) {
+                        while (true) {  // refill lanes with empty masks
+                            const bool need = tmask == 0;
+                            const uint64_t bal = ballot(need);
+                            if (!bal || next_edge >= n_edges) break;
+                            const int e = next_edge + mask_prefix(bal);
+                            if (need && e < n_edges) {
+                                const uint32_t ed = edges[e];
+                                ea = ed >> 8;
+                                eb = ed & 255;
+                                tmask = s.adj[ea] & s.adj[eb] & ((1ull << eb) - 1ull);
+                            }
+                            next_edge += __popcll(bal);
+                            if (ballot(tmask == 0) == 0) break;
                         }
-                        next_edge += __popcll(bal);
-                        if (ballot(tmask == 0) == 0) break;
+                        const bool active = tmask != 0;
+                        const uint64_t bal = ballot(active);
+                        if (!bal) break;
+                        if (active) {
+                            const int c = __ffsll((unsigned long long)tmask) - 1;
+                            tmask &= tmask - 1;
+                            tl[ntri + mask_prefix(bal)] = pack3(ea, eb, c);
+                        }
+                        ntri += __popcll(bal);
                     }
-                    const bool active = tmask != 0;
-                    if (!ballot(active)) break;
+                }
+                __syncthreads();  // the list (scratch) is read by other lanes
+                DGN_PHASE(26);
+                // (2b) one lane per column (uncleared triangle). Global reads leave the per-round
+                // dependency chain: list entries are fetched two rounds ahead, their clearing
+                // bytes one round ahead.
+                uint32_t tp1 = lane < ntri ? tl[lane] : 0u;
+                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
+                uint32_t tp2 = kWave + lane < ntri ? tl[kWave + lane] : 0u;
+                for (int base = 0; base < ntri; base += kWave) {
+                    const uint32_t tp = tp1, clb = cl1;
+                    const bool active = base + lane < ntri;
+                    tp1 = tp2;
+                    cl1 = base + kWave + lane < ntri
+                              ? (uint32_t)mincof[tri_dense((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
+                              : 0u;
+                    tp2 = base + 2 * kWave + lane < ntri ? tl[base + 2 * kWave + lane] : 0u;
                     bool apparent = false, na_col = false;
                     float birth = 0.f, death = 0.f;
                     uint64_t colkey = 0, best = kInf;
                     if (active) {
-                        const int a = ea, b = eb;
-                        const int c = __ffsll((unsigned long long)tmask) - 1;
-                        tmask &= tmask - 1;
+                        const int a = (tp >> 16) & 255, b = (tp >> 8) & 255, c = tp & 255;
                         uint32_t mc = kMcNone;
-                        if (!cx.is_cleared(a, b, c)) {
+                        if (clb != kMcCleared) {
                             birth = cx.tri_diam(a, b, c);
-                            colkey = make_key(birth, pack3(a, b, c));
+                            colkey = make_key(birth, tp);
                             const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
                             if (cand) {
                                 best = cx.min_cofacet_lane(2, a, b, c, birth, cand);
                                 death = key_diam(best);
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
-                                apparent = cx.max_facet(2, best) == pack3(a, b, c);
+                                apparent = cx.max_facet(2, best) == tp;
                                 na_col = !apparent;
-                                mc = extra_vertex(key_packed(best), pack3(a, b, c));
+                                mc = extra_vertex(key_packed(best), tp);
                             }
                         }
                         mincof[tri_dense(a, b, c)] = (uint8_t)mc;

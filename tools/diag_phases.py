@@ -34,7 +34,7 @@ ph = list(ph)
 names = ["load+gram", "adj+prim+edges", "dim1 apparent", "dim1 serial", "dim2 apparent", "dim2 serial",
          "stats+write", "dequeue/gap"]
 sub = ["serial:sort", "serial:col-start", "serial:find_pivot", "serial:apparent_owner", "serial:toggles", "serial:pivot_of_V", "serial:finalize"]
-tot = sum(ph[:8]) + sum(ph[16:23])
+tot = sum(ph[:8]) + sum(ph[16:23]) + ph[26]
 out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round(dt, 4),
        "betti_vr_ms": round(kt.get("betti_vr", {}).get("total_ms", 0.0), 3),
        "cycles_per_complex": round(tot / A), "phase_cycles_per_complex": {n: round(ph[i] / A) for i, n in enumerate(names)},
@@ -42,6 +42,6 @@ out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round
        "na1_per_complex": ph[8] / A, "na2_per_complex": ph[9] / A, "adds1": ph[10] / A, "adds2": ph[11] / A,
        "spills_per_complex": ph[12] / A, "dim2_complexes": ph[13],
        "pivot_V_entries_per_complex": ph[14] / A, "pivot_V_sq_per_complex": ph[15] / A,
-       "max_V": ph[23], "pivot_iters_per_complex": ph[24] / A, "pivot_iter_entries_per_complex": ph[25] / A, "d2_rounds": ph[28] / A, "d2_active_lanes": ph[29] / A, "d2_wave_groups": ph[26] / A, "d2_lane_groups": ph[27] / A,
-       "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
+       "max_V": ph[23], "pivot_iters_per_complex": ph[24] / A, "pivot_iter_entries_per_complex": ph[25] / A,
+       "dim2_enumerate_cycles_per_complex": round(ph[26] / A), "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
 print(json.dumps(out, indent=1))
