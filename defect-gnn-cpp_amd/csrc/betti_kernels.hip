@@ -1017,57 +1017,7 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                 continue;
             }
             // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
-            // group g: 0 d0 death | 1..3 d1 pers, birth, death | 4..6 d2 pers, birth, death
-            double myval = 0.0;
-#pragma unroll 1
-            for (int g = 0; g < 7; ++g) {
-                const int m = g == 0 ? cx.n_d0 : (g <= 3 ? cx.n_p1 : cx.n_p2);
-                double st[5] = {0, 0, 0, 0, 0};
-                if (m > 0) {
-                    const float2* P = g == 0 ? nullptr : cx.pairs(g <= 3 ? 1 : 2);
-                    const int which = g == 0 ? 1 : ((g - 1) % 3 == 0 ? 2 : ((g - 1) % 3 == 1 ? 0 : 1));
-                    double sum = 0.0, mx = -INFINITY, mn = INFINITY;
-                    for (int i = lane; i < m; i += kWave) {
-                        double v;
-                        if (g == 0) v = (double)s.d0[i];
-                        else {
-                            const float2 pr = P[i];
-                            const double bb = pr.x, dd = pr.y;
-                            v = which == 0 ? bb : (which == 1 ? dd : dd - bb);
-                        }
-                        sum += v;
-                        mx = fmax(mx, v);
-                        mn = fmin(mn, v);
-                    }
-                    sum = wave_sum(sum);
-                    mx = wave_max(mx);
-                    mn = wave_min(mn);
-                    const double mean = sum / (double)m;
-                    double ss = 0.0;
-                    for (int i = lane; i < m; i += kWave) {
-                        double v;
-                        if (g == 0) v = (double)s.d0[i];
-                        else {
-                            const float2 pr = P[i];
-                            const double bb = pr.x, dd = pr.y;
-                            v = which == 0 ? bb : (which == 1 ? dd : dd - bb);
-                        }
-                        ss += (v - mean) * (v - mean);
-                    }
-                    ss = wave_sum(ss);
-                    st[0] = mean;
-                    st[1] = sqrt(ss / (double)m);  // population std (math.hpp:13-16)
-                    st[2] = mx;
-                    st[3] = mn;
-                    st[4] = sum * weight;  // weighted_sum = sum * weight (math.hpp:26-28)
-                }
-                const int r = lane - 5 * g;
-                if (r == 0) myval = st[0];
-                if (r == 1) myval = st[1];
-                if (r == 2) myval = st[2];
-                if (r == 3) myval = st[3];
-                if (r == 4) myval = st[4];
-            }
+            const double myval = betti_stats35(s.d0, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
             if (feat && lane < 35) feat[lane] = myval;
             if (bl.pairs_out) {
                 float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;

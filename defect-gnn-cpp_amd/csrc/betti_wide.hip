@@ -675,56 +675,7 @@ struct WideCx {
         const float* d0s = sp<float>(ly.d0);
         const float2* P1 = sp<float2>(ly.p1);
         const float2* P2 = sp<float2>(ly.p2);
-        double myval = 0.0;
-#pragma unroll 1
-        for (int g = 0; g < 7; ++g) {
-            const int m = g == 0 ? n_d0 : (g <= 3 ? n_p1 : n_p2);
-            double st[5] = {0, 0, 0, 0, 0};
-            if (m > 0) {
-                const float2* P = g <= 3 ? P1 : P2;
-                const int which = g == 0 ? 1 : ((g - 1) % 3 == 0 ? 2 : ((g - 1) % 3 == 1 ? 0 : 1));
-                double sum = 0.0, mx = -INFINITY, mn = INFINITY;
-                for (int i = lane; i < m; i += kWave) {
-                    double v;
-                    if (g == 0) {
-                        v = (double)d0s[i];
-                    } else {
-                        const float2 pr = P[i];
-                        v = which == 0 ? (double)pr.x : (which == 1 ? (double)pr.y : (double)pr.y - (double)pr.x);
-                    }
-                    sum += v;
-                    mx = fmax(mx, v);
-                    mn = fmin(mn, v);
-                }
-                sum = wave_sum(sum);
-                mx = wave_max(mx);
-                mn = wave_min(mn);
-                const double mean = sum / (double)m;
-                double ss = 0.0;
-                for (int i = lane; i < m; i += kWave) {
-                    double v;
-                    if (g == 0) {
-                        v = (double)d0s[i];
-                    } else {
-                        const float2 pr = P[i];
-                        v = which == 0 ? (double)pr.x : (which == 1 ? (double)pr.y : (double)pr.y - (double)pr.x);
-                    }
-                    ss += (v - mean) * (v - mean);
-                }
-                ss = wave_sum(ss);
-                st[0] = mean;
-                st[1] = sqrt(ss / (double)m);  // population std (math.hpp:13-16)
-                st[2] = mx;
-                st[3] = mn;
-                st[4] = sum * weight;  // weighted_sum = sum * weight (math.hpp:26-28)
-            }
-            const int r = lane - 5 * g;
-            if (r == 0) myval = st[0];
-            if (r == 1) myval = st[1];
-            if (r == 2) myval = st[2];
-            if (r == 3) myval = st[3];
-            if (r == 4) myval = st[4];
-        }
+        const double myval = betti_stats35(d0s, n_d0, P1, n_p1, P2, n_p2, weight);
         if (feat && lane < 35) feat[lane] = myval;
         if (bl.pairs_out) {
             float2* po = reinterpret_cast<float2*>(bl.pairs_out) + gi * 3 * bl.pair_cap;

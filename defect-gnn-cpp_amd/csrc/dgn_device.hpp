@@ -68,4 +68,78 @@ __device__ __forceinline__ T wave_inclusive_sum(T v) {
 
 __device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
+// ---- DPP wave reductions of doubles: row_ror 1/2/4/8 inside each 16-lane row (VALU latency,
+// no LDS round trips), then the four row results by v_readlane ----
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+struct OpAdd { __device__ static double f(double a, double b) { return a + b; } };
+struct OpMax { __device__ static double f(double a, double b) { return fmax(a, b); } };
+struct OpMin { __device__ static double f(double a, double b) { return fmin(a, b); } };
+template <class Op>
+__device__ __forceinline__ double wave_reduce_f64(double v) {
+    v = Op::f(v, dpp_f64<0x121>(v));
+    v = Op::f(v, dpp_f64<0x122>(v));
+    v = Op::f(v, dpp_f64<0x124>(v));
+    v = Op::f(v, dpp_f64<0x128>(v));
+    return Op::f(Op::f(readlane_f64(v, 0), readlane_f64(v, 16)), Op::f(readlane_f64(v, 32), readlane_f64(v, 48)));
+}
+
+// The 35 Betti statistics of one atom (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28):
+// groups 0 dim-0 death | 1..3 dim-1 persistence, birth, death | 4..6 dim-2 persistence, birth,
+// death; each mean, population std (two-pass), max, min, sum * weight; zeros for an empty
+// diagram. One group at a time (few live uniform values), DPP reductions (no LDS round trips).
+// Returns feature `lane` for lanes < 35.
+__device__ __forceinline__ double betti_stats35(const float* d0, int n0, const float2* P1, int n1, const float2* P2,
+                                                int n2, double weight) {
+    const int lane = lane_id();
+    double out = 0.0;
+#pragma unroll 1
+    for (int g = 0; g < 7; ++g) {
+        const int m = g == 0 ? n0 : (g <= 3 ? n1 : n2);
+        if (m == 0) continue;
+        const float2* P = g <= 3 ? P1 : P2;
+        const int which = g == 0 ? 1 : (g - 1) % 3;  // 0 persistence, 1 birth, 2 death (dims 1, 2)
+        auto val = [&](int i) -> double {
+            if (g == 0) return (double)d0[i];
+            const float2 pr = P[i];
+            return which == 0 ? (double)pr.y - (double)pr.x : (which == 1 ? (double)pr.x : (double)pr.y);
+        };
+        double sm = 0.0, mx = -INFINITY, mn = INFINITY;
+        for (int i = lane; i < m; i += kWave) {
+            const double v = val(i);
+            sm += v;
+            mx = fmax(mx, v);
+            mn = fmin(mn, v);
+        }
+        sm = wave_reduce_f64<OpAdd>(sm);
+        mx = wave_reduce_f64<OpMax>(mx);
+        mn = wave_reduce_f64<OpMin>(mn);
+        const double mean = sm / (double)m;
+        double ss = 0.0;
+        for (int i = lane; i < m; i += kWave) {
+            const double v = val(i);
+            ss += (v - mean) * (v - mean);
+        }
+        ss = wave_reduce_f64<OpAdd>(ss);
+        const int r = lane - 5 * g;
+        if (r == 0) out = mean;
+        if (r == 1) out = sqrt(ss / (double)m);  // population std (math.hpp:13-16)
+        if (r == 2) out = mx;
+        if (r == 3) out = mn;
+        if (r == 4) out = sm * weight;  // weighted_sum = sum * weight (math.hpp:26-28)
+    }
+    return out;
+}
+
 }  // namespace dgn
