@@ -210,16 +210,40 @@ struct WideCx {
         found = false;
         bk = 0;
         bestp = 0;
+        // candidates popped highest first, four per step so their distance reads are in flight
+        // together (scratch reads: the latency, not the bandwidth, is what a lane waits for)
+        int w = W - 1;
+        uint64_t m = cand[W - 1];
+        for (;;) {
+            int kk[4];
+            bool val[4];
 #pragma unroll
-        for (int w = kWW - 1; w >= 0; --w) {
-            if (w >= W || found) continue;
-            uint64_t m = cand[w];
-            while (m) {
-                const int bit = 63 - __clzll((long long)m);
-                m &= ~(1ull << bit);
-                const int k = 64 * w + bit;
-                const uint32_t da = d(a, k), db_ = d(b, k), dc = dim == 2 ? d(c, k) : 0u;
-                const uint32_t dk = max(max(da, db_), dc);
+            for (int j = 0; j < 4; ++j) {
+                while (m == 0ull && w > 0) {
+                    --w;
+#pragma unroll
+                    for (int u = 0; u < kWW; ++u)
+                        if (u == w) m = cand[u];
+                }
+                val[j] = m != 0ull;
+                const int bit = val[j] ? 63 - __clzll((long long)m) : 0;
+                kk[j] = 64 * w + bit;
+                if (val[j]) m &= ~(1ull << bit);
+            }
+            if (!val[0]) break;
+            uint32_t da[4], dbv[4], dc[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int k = val[j] ? kk[j] : kk[0];
+                da[j] = d(a, k);
+                dbv[j] = d(b, k);
+                dc[j] = dim == 2 ? d(c, k) : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!val[j] || found) continue;
+                const int k = kk[j];
+                const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
                 const uint64_t p = pinsert(dim + 1, sp_, k);
                 const uint64_t idx = pidx(dim + 2, p);
                 if (dk <= dsig) {
@@ -227,18 +251,19 @@ struct WideCx {
                     bestp = p;
                     bk = k;
                     found = true;
-                    hda = da;
-                    hdb = db_;
-                    hdc = dc;
-                    break;
-                }
-                const uint64_t kk = wkey(dk, idx);
-                if (kk < best) {
-                    best = kk;
-                    bestp = p;
-                    bk = k;
+                    hda = da[j];
+                    hdb = dbv[j];
+                    hdc = dc[j];
+                } else {
+                    const uint64_t kk2 = wkey(dk, idx);
+                    if (kk2 < best) {
+                        best = kk2;
+                        bestp = p;
+                        bk = k;
+                    }
                 }
             }
+            if (found || !val[3]) break;
         }
         return best;
     }
@@ -692,15 +717,42 @@ struct WideCx {
     }
 
     __device__ void run(int64_t gi, double weight) {
+#ifdef DGN_PHASE_TIMING
+        // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
+        uint64_t t0 = __builtin_amdgcn_s_memtime();
+        auto stamp = [&](int k) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane_id() == 0 && bl.phase_cycles) atomicAdd(&bl.phase_cycles[k], (unsigned long long)(t - t0));
+            t0 = t;
+        };
+#define WSTAMP(k) stamp(k)
+#else
+#define WSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
         load(gi);
+        WSTAMP(0);
         prim();
         const int n_edges = edge_list();
+        WSTAMP(1);
         const int nna1 = pass_dim1(n_edges);
+        WSTAMP(2);
         reduce(1, nna1);
+        WSTAMP(3);
         __syncthreads();  // clearing marks complete before the dim-2 pass reads them
         if (err == 0u) {
             const int nna2 = pass_dim2(n_edges);
+            WSTAMP(4);
             reduce(2, nna2);
+            WSTAMP(5);
+#ifdef DGN_PHASE_TIMING
+            if (lane_id() == 0 && bl.phase_cycles) {
+                atomicAdd(&bl.phase_cycles[8], (unsigned long long)nna1);
+                atomicAdd(&bl.phase_cycles[9], (unsigned long long)nna2);
+                atomicAdd(&bl.phase_cycles[10], (unsigned long long)n_edges);
+            }
+#endif
         } else {
             // no dim-2 pass consumes the clearing marks: erase every triangle entry
             uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
@@ -710,6 +762,8 @@ struct WideCx {
         __syncthreads();
         finish(gi, weight);
         __syncthreads();
+        WSTAMP(6);
+#undef WSTAMP
     }
 };
 
