@@ -1067,13 +1067,20 @@ __global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLau
             n = (int)(bl.row_ptr[gi + 1] - r0) + 1;
         }
         if (lane == 0) dl.npoints[c] = n;
-        // 1/count(species) of the centre's structure (betti_features.cpp:62-63, 77)
+        // 1/count(species) of the centre's structure (betti_features.cpp:62-63, 77); the structure
+        // comes from the atom -> structure map of the neighbour pass
         if (bl.species) {
-            int64_t lo = 0, hi = bl.num_structures - 1;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi + 1) >> 1;
-                if (bl.atom_offset[mid] <= gi) lo = mid;
-                else hi = mid - 1;
+            int64_t lo;
+            if (bl.atom_struct) {
+                lo = bl.atom_struct[gi];
+            } else {
+                lo = 0;
+                int64_t hi = bl.num_structures - 1;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi + 1) >> 1;
+                    if (bl.atom_offset[mid] <= gi) lo = mid;
+                    else hi = mid - 1;
+                }
             }
             const int64_t s0 = bl.atom_offset[lo], s1 = bl.atom_offset[lo + 1];
             const int spc = bl.species[gi];

@@ -352,6 +352,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.pos = given ? nullptr : b->positions;
     bl.species = given ? nullptr : b->species;
     bl.atom_offset = given ? nullptr : b->atom_offset;
+    bl.atom_struct = given ? nullptr : c->atom_struct.as<int32_t>();  // written by graph_count_impl
     bl.num_structures = given ? 0 : b->num_structures;
     bl.num_atoms = A;
     bl.thr = (float)rc;  // ripser_wrapper.cpp:28
@@ -401,7 +402,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     } else {
         // distance pass (MFMA) + Betti pass per chunk of complexes; the triangle buffer is
         // bounded (~16 GB of the 288 GB HBM) so arbitrarily large shards stream through it
-        const int64_t tri_stride = std::max<int64_t>(1, (int64_t)max_points * (max_points - 1) / 2);
+        // floats per complex, padded to a multiple of 4 (16-byte aligned complexes)
+        const int64_t tri_stride = std::max<int64_t>(4, ((int64_t)max_points * (max_points - 1) / 2 + 3) / 4 * 4);
         const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(16) << 30) / (4 * tri_stride)));
         bl.tri_stride = tri_stride;  // the distance pass writes [chunk][tri_stride]
         HIP_TRY(c, c->b_lower.ensure(sizeof(float) * (size_t)(chunk * tri_stride)));

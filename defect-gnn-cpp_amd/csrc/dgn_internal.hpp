@@ -64,6 +64,7 @@ struct BettiLaunch {
     const double* pos;        // [A][3]
     const int32_t* species;   // [A]
     const int64_t* atom_offset;
+    const int32_t* atom_struct;  // atom -> structure (from the neighbour pass) or null
     int64_t num_structures, num_atoms;
     float thr;                // (float) r_cutoff
     double* features;         // [A][35]
