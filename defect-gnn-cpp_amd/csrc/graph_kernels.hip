@@ -600,7 +600,10 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_rows_kernel(
                     ++le;
                 }
             }
-            *reinterpret_cast<float4*>(out + f) = make_float4(o[0], o[1], o[2], o[3]);
+            // streaming (non-temporal) 16-byte store: the RBF block is written once, never re-read here
+            typedef float float4_t __attribute__((ext_vector_type(4)));
+            const float4_t ov = {o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(ov, reinterpret_cast<float4_t*>(out + f));
         }
         const int t0 = head + 4 * nvec;
         if (t0 + tid < total) {
@@ -626,7 +629,9 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_rows_kernel(
                     ++le;
                 }
             }
-            *reinterpret_cast<double2*>(out + f) = make_double2(o[0], o[1]);
+            typedef double double2_t __attribute__((ext_vector_type(2)));
+            const double2_t ov = {o[0], o[1]};
+            __builtin_nontemporal_store(ov, reinterpret_cast<double2_t*>(out + f));
         }
         const int t0 = head + 2 * nvec;
         if (t0 + tid < total) {
