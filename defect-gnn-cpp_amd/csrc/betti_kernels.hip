@@ -38,6 +38,10 @@ constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
 constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
 constexpr int kChunk = 4;         // complexes per dequeue
+#ifndef DGN_PV_UNROLL
+#define DGN_PV_UNROLL 4
+#endif
+constexpr int kPvUnroll = DGN_PV_UNROLL;  // V entries per step of the pivot search
 
 constexpr uint64_t kInf = ~0ull;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -118,30 +122,22 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
     return ((uint64_t)hi << 32) | lo;
 }
-// min over the wave of a 64-bit key, DPP row rotations (VALU latency) + 4 readlanes
+// min over the wave of a 64-bit key in two 32-bit stages: the high words (DPP row rotations +
+// 4 readlanes), then the low words of the lanes holding that high word
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x121, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x122, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x124, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xf, 0xf, false));
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return min(min(a, b), min(c, d));
+}
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#define DGN_MIN_STEP(ctrl)                                                          \
-    {                                                                               \
-        const uint32_t l2 = (uint32_t)__builtin_amdgcn_update_dpp((int)lo, (int)lo, ctrl, 0xf, 0xf, false); \
-        const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp((int)hi, (int)hi, ctrl, 0xf, 0xf, false); \
-        const bool take = (h2 < hi) || (h2 == hi && l2 < lo);                       \
-        lo = take ? l2 : lo;                                                        \
-        hi = take ? h2 : hi;                                                        \
-    }
-    DGN_MIN_STEP(0x121)  // row_ror:1
-    DGN_MIN_STEP(0x122)  // row_ror:2
-    DGN_MIN_STEP(0x124)  // row_ror:4
-    DGN_MIN_STEP(0x128)  // row_ror:8
-#undef DGN_MIN_STEP
-    uint64_t best = kInf;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const uint64_t x = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
-        best = x < best ? x : best;
-    }
-    return best;
+    const uint32_t hi = (uint32_t)(v >> 32);
+    const uint32_t mh = wave_min_u32(hi);
+    const uint32_t ml = wave_min_u32(hi == mh ? (uint32_t)v : 0xFFFFFFFFu);
+    return ((uint64_t)mh << 32) | ml;
 }
 
 // F-order key: ascending key == Ripser's filtration order (diameter ascending, then the
@@ -254,68 +250,56 @@ struct Complex {
         np += __popcll(bal);
     }
 
-    // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand.
-    // Inserting a larger vertex k gives a larger packed tuple, i.e. an F-smaller key among
-    // cofacets of equal diameter; so walking k downwards, the first k whose distances to the
-    // simplex are all <= diam yields the F-minimal cofacet (diameter diam, largest index)
-    // and ends the search. Cofacets seen before it have larger diameters.
-    __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, float diam, uint64_t cand) const {
-        uint64_t best = kInf;
-        const uint32_t dbits = __float_as_uint(diam);
-        const uint32_t abc = dim == 1 ? pack2(a, b) : pack3(a, b, c);
+    // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand (kInf if
+    // cand is empty). For one simplex, inserting a larger vertex k gives a larger packed tuple,
+    // i.e. an F-smaller key among cofacets of equal diameter; so walking k downwards, a later
+    // (smaller) k wins only with a strictly smaller diameter, and the first k whose distances to
+    // the simplex are all <= its diameter is the F-minimal cofacet and ends the search (found).
+    // Only the winner's packed tuple is built. bk = the inserted vertex; when found, hda/hdb/hdc
+    // are its distances to a, b, c, so the apparent test needs no further reads.
+    __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, uint32_t dbits, uint64_t cand, int& bk,
+                                         bool& found, uint32_t& hda, uint32_t& hdb, uint32_t& hdc) const {
+        uint32_t bd = 0xFFFFFFFFu;  // diameter of the best cofacet so far
+        bk = -1;
+        found = false;
+        hda = hdb = hdc = 0u;
+        const uint32_t* ra = Db() + a * S;  // rows a, b, c: entry k is d(., k)
+        const uint32_t* rb = Db() + b * S;
+        const uint32_t* rcv = Db() + c * S;
         // four candidates per step (descending), their distance reads issued together
         while (cand) {
             int kk[4];
             bool val[4];
-            uint32_t dk[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 val[j] = cand != 0;
                 kk[j] = val[j] ? 63 - __clzll((long long)cand) : 0;
-                cand &= ~(1ull << kk[j]) | (val[j] ? 0ull : ~0ull);
+                cand &= val[j] ? ~(1ull << kk[j]) : ~0ull;
+            }
+            uint32_t da[4], dbb[4], dc[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                da[j] = ra[kk[j]];
+                dbb[j] = rb[kk[j]];
+                dc[j] = dim == 2 ? rcv[kk[j]] : 0u;
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int k = kk[j];
-                dk[j] = max(db(a, k), db(b, k));
-                if (dim == 2) dk[j] = max(dk[j], db(c, k));
-            }
-            bool found = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t uk = (uint32_t)kk[j];
-                uint32_t pk;
-                if (dim == 1) {
-                    const uint32_t p1 = pin((uk << 16) | abc);
-                    const uint32_t p2 = pin(((uint32_t)a << 16) | (uk << 8) | (uint32_t)b);
-                    const uint32_t p3 = pin((abc << 8) | uk);
-                    pk = kk[j] > a ? p1 : (kk[j] > b ? p2 : p3);
-                } else {
-                    const uint32_t p1 = pin((uk << 24) | abc);
-                    const uint32_t p2 = pin(((uint32_t)a << 24) | (uk << 16) | (abc & 0xFFFFu));
-                    const uint32_t p3 = pin(((abc >> 8) << 16) | (uk << 8) | (uint32_t)c);
-                    const uint32_t p4 = pin((abc << 8) | uk);
-                    pk = kk[j] > a ? p1 : (kk[j] > b ? p2 : (kk[j] > c ? p3 : p4));
-                }
-                const bool hit = val[j] && !found && dk[j] <= dbits;
-                const uint64_t key = ((uint64_t)(hit ? dbits : dk[j]) << 32) | (uint64_t)(~pk);
-                best = (val[j] && !found && key < best) ? key : best;
+                const uint32_t dk = max(max(da[j], dbb[j]), max(dc[j], dbits));  // cofacet diameter
+                const bool take = val[j] && !found && dk < bd;
+                const bool hit = take && dk == dbits;
+                bd = take ? dk : bd;
+                bk = take ? kk[j] : bk;
+                hda = hit ? da[j] : hda;
+                hdb = hit ? dbb[j] : hdb;
+                hdc = hit ? dc[j] : hdc;
                 found = found || hit;
             }
             if (found) break;
         }
-        return best;
-    }
-
-    // whole wave: F-minimal cofacet, lane k evaluates vertex k
-    __device__ uint64_t min_cofacet_wave(int dim, int a, int b, int c, float diam, uint64_t cand) const {
-        const int k = lane_id();
-        uint64_t key = kInf;
-        if ((cand >> k) & 1ull) {
-            if (dim == 1) key = make_key(fmaxf(diam, fmaxf(dist(a, k), dist(b, k))), tri_with(a, b, k));
-            else key = make_key(fmaxf(diam, fmaxf(fmaxf(dist(a, k), dist(b, k)), dist(c, k))), tet_with(a, b, c, k));
-        }
-        return wave_min_u64(key);
+        if (bk < 0) return kInf;
+        const uint32_t pk = dim == 1 ? tri_with(a, b, bk) : tet_with(a, b, c, bk);
+        return ((uint64_t)bd << 32) | (uint64_t)(~pk);
     }
 
     // F-max facet of pivot tau as (packed vertices)
@@ -399,7 +383,6 @@ struct Complex {
     // refreshes the diameters lane-parallel and reads entries back uniformly with v_readlane.
     uint32_t vs0 = 0, vs1 = 0;
     float vd0 = 0.f, vd1 = 0.f;
-    uint64_t myadj = 0;  // lane k: adjacency row of vertex k (cofacet candidates test bits of it)
 
     __device__ static uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
     __device__ static uint64_t rl64(uint64_t x, int l) {
@@ -454,11 +437,9 @@ struct Complex {
         const int a = dim == 1 ? (int)((sp_ >> 8) & 255) : (int)((sp_ >> 16) & 255);
         const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
         const int c = (int)(sp_ & 255);
-        const bool on = dim == 1 ? ((myadj >> a) & (myadj >> b) & 1ull) != 0
-                                 : ((myadj >> a) & (myadj >> b) & (myadj >> c) & 1ull) != 0;
         // lane k reads row entries (x, k): consecutive lanes, consecutive banks. Lanes with
         // k >= NP read past the matrix into adj/tree (still inside the struct) and are masked
-        // off by `on`. Every select arm is materialized (pin): v_cndmask, never exec branches.
+        // off by k < n. Every select arm is materialized (pin): v_cndmask, never exec branches.
         uint32_t dd = max(__float_as_uint(diam), max(Db()[a * S + k], Db()[b * S + k]));
         uint32_t pk;
         const uint32_t uk = (uint32_t)k;
@@ -479,7 +460,17 @@ struct Complex {
             pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
         }
         const uint64_t key = ((uint64_t)dd << 32) | (uint64_t)(~pk);
-        return (on && key > floor) ? key : kInf;
+        // k is a common neighbour iff every distance to it is <= thr (sparse_distance_matrix):
+        // the diameter bound covers it, the +inf diagonal excludes k in the simplex, and lanes
+        // k >= n (reading past the row) are not vertices
+        return (k < n && dd <= __float_as_uint(thr) && key > floor) ? key : kInf;
+    }
+
+    // lane k's key of the cofacet (V entry e) u {k} above floor (e wave-uniform)
+    __device__ uint64_t entry_key(int dim, int k, int e, uint64_t floor) const {
+        const uint32_t sx = e < 64 ? rl(vs0, e) : rl(vs1, e - 64);
+        const uint32_t dx = e < 64 ? rl(__float_as_uint(vd0), e) : rl(__float_as_uint(vd1), e - 64);
+        return cofacet_key_above(dim, k, sx, __uint_as_float(dx), floor);
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
@@ -492,18 +483,21 @@ struct Complex {
     __device__ uint64_t pivot_of_V(int dim, int v_, uint64_t floor) {
         const int k = lane_id();
         const int v = (int)uni((uint32_t)v_);
-        const int v0 = v < 64 ? v : 64;
         if (k < v) vd0 = simplex_diam(dim, vs0);
         if (v > 64 && k + 64 < v) vd1 = simplex_diam(dim, vs1);
         for (;;) {
             uint64_t lmin = kInf;
-            for (int i = 0; i < v0; ++i) {
-                const uint64_t key = cofacet_key_above(dim, k, rl(vs0, i), __uint_as_float(rl(__float_as_uint(vd0), i)), floor);
-                lmin = key < lmin ? key : lmin;
+            // kPvUnroll V entries per step, their distance reads in flight together, then the rest
+            int i = 0;
+            for (; i + kPvUnroll <= v; i += kPvUnroll) {
+                uint64_t kq[kPvUnroll];
+#pragma unroll
+                for (int u = 0; u < kPvUnroll; ++u) kq[u] = entry_key(dim, k, i + u, floor);
+#pragma unroll
+                for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
             }
-            for (int i = 64; i < v; ++i) {
-                const uint64_t key =
-                    cofacet_key_above(dim, k, rl(vs1, i - 64), __uint_as_float(rl(__float_as_uint(vd1), i - 64)), floor);
+            for (; i < v; ++i) {
+                const uint64_t key = entry_key(dim, k, i, floor);
                 lmin = key < lmin ? key : lmin;
             }
             const uint64_t m = wave_min_u64(lmin);
@@ -532,7 +526,6 @@ struct Complex {
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
         if (nna > kNACap) { err |= kErrNA; return; }
-        myadj = lane < n ? s.adj[lane] : 0ull;
         const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
         const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
         const bool regs = nna <= 2 * kWave;
@@ -701,7 +694,7 @@ struct Complex {
 #endif
 
 template <int NP>
-__global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
+__global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
     __shared__ int64_t chunk_s;
 #ifdef DGN_PHASE_TIMING
@@ -711,6 +704,8 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();
+    // +inf diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key_above)
+    if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0x7F800000u);
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;
 
@@ -864,17 +859,24 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                             colkey = make_key(birth, pack2(i, j));
                             const uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
-                                best = cx.min_cofacet_lane(1, i, j, 0, birth, cand);
+                                const uint32_t dij = __float_as_uint(birth);
+                                int bk;
+                                bool found;
+                                uint32_t hda, hdb, hdc;
+                                best = cx.min_cofacet_lane(1, i, j, 0, dij, cand, bk, found, hda, hdb, hdc);
                                 death = key_diam(best);
-                                // apparent iff (i,j) is the F-max facet of its pivot triangle
-                                apparent = cx.max_facet(1, best) == pack2(i, j);
+                                // apparent iff (i,j) is the F-max facet of its pivot triangle: a
+                                // zero-persistence cofacet whose other facets (bk replacing i or j)
+                                // are shorter, or as long with a larger index (bk above the
+                                // replaced vertex)
+                                apparent = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
                                 if (apparent) {
                                     const uint32_t tp = key_packed(best);
                                     cx.set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
                                 } else {
                                     na_col = true;
                                 }
-                                mc = extra_vertex(key_packed(best), pack2(i, j));
+                                mc = (uint32_t)bk;
                             }
                         }
                         mincof_e[edge_dense(i, j)] = (uint8_t)mc;
@@ -968,16 +970,24 @@ __global__ __launch_bounds__(kWave, 3) void betti_kernel(BettiLaunch bl) {
                         const int a = (tp >> 16) & 255, b = (tp >> 8) & 255, c = tp & 255;
                         uint32_t mc = kMcNone;
                         if (clb != kMcCleared) {
-                            birth = cx.tri_diam(a, b, c);
+                            const uint32_t dab = cx.dlowb(a, b), dac = cx.dlowb(a, c), dbc = cx.dlowb(b, c);
+                            const uint32_t ds = max(max(dab, dac), dbc);
+                            birth = __uint_as_float(ds);
                             colkey = make_key(birth, tp);
                             const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
                             if (cand) {
-                                best = cx.min_cofacet_lane(2, a, b, c, birth, cand);
+                                int bk;
+                                bool found;
+                                uint32_t hda, hdb, hdc;
+                                best = cx.min_cofacet_lane(2, a, b, c, ds, cand, bk, found, hda, hdb, hdc);
                                 death = key_diam(best);
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
-                                apparent = cx.max_facet(2, best) == tp;
+                                // (the dim-1 facet test, one facet per replaced vertex)
+                                apparent = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
+                                           (bk > b || max(max(hda, hdc), dac) < ds) &&
+                                           (bk > c || max(max(hda, hdb), dab) < ds);
                                 na_col = !apparent;
-                                mc = extra_vertex(key_packed(best), tp);
+                                mc = (uint32_t)bk;
                             }
                         }
                         mincof[tri_dense(a, b, c)] = (uint8_t)mc;

@@ -6,8 +6,9 @@
 // then have ~340 points. betti_kernels.hip covers n <= 64 with
 // one lane per vertex and the complex in LDS; this kernel runs the same algorithm with the
 // same output contract on larger complexes:
-//   * vertex sets are multi-word bitsets in LDS (kWW 64-bit words per vertex); lane k handles
-//     vertices k, k + 64, ...;
+//   * vertex sets are multi-word bitsets in LDS (W = ceil(n / 64) 64-bit words per vertex; the
+//     dynamic LDS block is sized by the launch's largest complex, so smaller cutoffs keep more
+//     waves resident); lane k handles vertices k, k + 64, ...;
 //   * the f32 distance matrix is stored full and row-major in per-wave scratch, so the
 //     lane-per-vertex reads of one row are coalesced;
 //   * simplices are named by their combinatorial index (Ripser's colex numbering,
@@ -72,8 +73,8 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 struct WideCx {
     const BettiLaunch& bl;
     const WideLayout& ly;
-    uint64_t* adj;  // LDS [kWideMaxPoints][kWW]
-    uint16_t* par;  // LDS [kWideMaxPoints]: spanning-forest parent, 0xFFFF = root
+    uint64_t* adj;  // LDS [n][W]: row v = the neighbours of vertex v, W words
+    uint16_t* par;  // LDS [n]: spanning-forest parent, 0xFFFF = root
     uint8_t* scr;
     int n, W;
     float thr;
@@ -83,7 +84,7 @@ struct WideCx {
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
     __device__ uint32_t d(int i, int j) const { return sp<uint32_t>(ly.D)[(int64_t)i * n + j]; }
-    __device__ uint64_t aw(int v, int w) const { return adj[v * kWW + w]; }
+    __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
     __device__ bool is_tree(int i, int j) const { return par[i] == j || par[j] == i; }
     __device__ uint32_t sdiam(int dim, uint64_t p) const {  // dim 1: edge, dim 2: triangle
         if (dim == 1) return d(pv(p, 1), pv(p, 0));
@@ -95,7 +96,7 @@ struct WideCx {
         const int lane = lane_id();
         const float* L = bl.lower + gi * bl.tri_stride;
         float* D = sp<float>(ly.D);
-        for (int i = lane; i < n * kWW; i += kWave) adj[i] = 0ull;
+        for (int i = lane; i < n * W; i += kWave) adj[i] = 0ull;
         for (int i = lane; i < n; i += kWave) D[(int64_t)i * n + i] = 0.0f;
         wave_lds_order();
         for (int i = 1; i < n; ++i) {
@@ -109,8 +110,8 @@ struct WideCx {
                     e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
                 }
                 const uint64_t b = ballot(e);
-                if (lane == 0) adj[i * kWW + (j0 >> 6)] = b;  // row i, columns j < i
-                if (e) atomicOr((unsigned long long*)&adj[j * kWW + (i >> 6)], 1ull << (i & 63));
+                if (lane == 0) adj[i * W + (j0 >> 6)] = b;  // row i, columns j < i
+                if (e) atomicOr((unsigned long long*)&adj[j * W + (i >> 6)], 1ull << (i & 63));
             }
         }
         __syncthreads();
@@ -768,9 +769,13 @@ struct WideCx {
 };
 
 __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
-    __shared__ uint64_t adj[kWideMaxPoints * kWW];
-    __shared__ uint16_t par[kWideMaxPoints];
-    __shared__ int64_t q_s;
+    // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
+    // [nmax] u16, the dequeue slot
+    extern __shared__ uint64_t wide_lds[];
+    const int64_t ww = (ly.nmax + 63) / 64;
+    uint64_t* adj = wide_lds;
+    uint16_t* par = reinterpret_cast<uint16_t*>(wide_lds + ly.nmax * ww);
+    int64_t& q_s = *reinterpret_cast<int64_t*>(wide_lds + ly.nmax * ww + (ly.nmax + 3) / 4);
     const int lane = lane_id();
     uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
     const int64_t total = (int64_t)*bl.wide_len;
@@ -794,6 +799,11 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
 }
 
 int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+size_t wide_lds_bytes(int nmax) {
+    const int64_t ww = (nmax + 63) / 64;
+    return (size_t)(8 * (nmax * ww + (nmax + 3) / 4 + 1));
+}
 
 }  // namespace
 
@@ -837,9 +847,21 @@ WideLayout betti_wide_layout(int nmax) {
     return l;
 }
 
+// waves of betti_wide_kernel resident on the whole device for complexes of up to nmax points
+int betti_wide_resident_waves(int device, int nmax) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_wide_kernel, kWave, wide_lds_bytes(nmax)) !=
+            hipSuccess ||
+        per_cu <= 0)
+        per_cu = 2;
+    return prop.multiProcessorCount * per_cu;
+}
+
 hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
     if (waves <= 0) return hipSuccess;
-    hipLaunchKernelGGL(betti_wide_kernel, dim3((unsigned)waves), dim3(kWave), 0, st, b, l);
+    hipLaunchKernelGGL(betti_wide_kernel, dim3((unsigned)waves), dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
     return hipGetLastError();
 }
 

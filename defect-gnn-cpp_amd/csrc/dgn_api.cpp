@@ -330,8 +330,14 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     int wide_waves = 0;
     if (max_points > 64) {
         wl = betti_wide_layout(max_points);
-        const int64_t budget = int64_t(8) << 30;
-        wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, 512, A}));
+        // as many waves as the device keeps resident (dynamic LDS sized by max_points), each
+        // with its own scratch, within half of the free HBM (288 GB per MI355X; at least 8 GB)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        const int64_t budget =
+            std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
+        const int64_t resident = betti_wide_resident_waves(c->device, max_points);
+        wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));

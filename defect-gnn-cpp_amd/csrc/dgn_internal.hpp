@@ -111,6 +111,7 @@ struct WideLayout {
 };
 WideLayout betti_wide_layout(int nmax);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
+int betti_wide_resident_waves(int device, int nmax);  // device-wide resident waves (occupancy API)
 
 // distance pass over complexes [first, first + count) of a BettiLaunch's CSR / cloud input
 struct DistLaunch {

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build a variant of libdgn.so with extra compile flags (A/B experiments; never used by tests):
+#   bash tools/build_variant.sh <tag> "-DFOO=1 ..."  -> defect-gnn-cpp_amd/lib/libdgn_<tag>.so
+set -eo pipefail
+TAG=$1; FLAGS=${2:-}
+cd "$(dirname "$0")/.."
+B=defect-gnn-cpp_amd/build_var_$TAG
+mkdir -p "$B"
+HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Idefect-gnn-cpp_amd/csrc -Iinclude $FLAGS"
+for f in graph_kernels betti_kernels betti_wide; do
+  /opt/rocm/bin/hipcc $HF -c defect-gnn-cpp_amd/csrc/$f.hip -o $B/$f.o &
+done
+/opt/rocm/bin/hipcc $HF -x hip -c defect-gnn-cpp_amd/csrc/dgn_api.cpp -o $B/dgn_api.o &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o defect-gnn-cpp_amd/lib/libdgn_$TAG.so $B/*.o
