@@ -125,10 +125,10 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
 // min over the wave of a 64-bit key in two 32-bit stages: the high words (DPP row rotations +
 // 4 readlanes), then the low words of the lanes holding that high word
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x121, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x122, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x124, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xf, 0xf, false));
     const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
     return min(min(a, b), min(c, d));
@@ -430,17 +430,16 @@ struct Complex {
     // tau in V, always in a different lane (k = tau \ s), so the multiplicity of the wave
     // minimum is the popcount of a ballot. Even multiplicity: raise the floor and repeat.
     // kInf for the zero column.
-    // key of the cofacet s u {k} for lane k (kInf if k is not a common neighbour of s or the
-    // key is not above floor). Branch-free: the lower-triangle index of (k, x) is
-    // c2(max) + min, so no lane-divergent selects between scalar and vector arms.
-    __device__ uint64_t cofacet_key_above(int dim, int k, uint32_t sp_, float diam, uint64_t floor) const {
+    // key of the cofacet s u {k} for lane k; its high word is 0xFFFFFFFF (above every real key)
+    // if k is not a common neighbour of s. Branch-free: every select is a v_cndmask.
+    __device__ uint64_t cofacet_key(int dim, int k, uint32_t sp_, uint32_t ds) const {
         const int a = dim == 1 ? (int)((sp_ >> 8) & 255) : (int)((sp_ >> 16) & 255);
         const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
         const int c = (int)(sp_ & 255);
         // lane k reads row entries (x, k): consecutive lanes, consecutive banks. Lanes with
         // k >= NP read past the matrix into adj/tree (still inside the struct) and are masked
         // off by k < n. Every select arm is materialized (pin): v_cndmask, never exec branches.
-        uint32_t dd = max(__float_as_uint(diam), max(Db()[a * S + k], Db()[b * S + k]));
+        uint32_t dd = max(ds, max(Db()[a * S + k], Db()[b * S + k]));
         uint32_t pk;
         const uint32_t uk = (uint32_t)k;
         if (dim == 1) {
@@ -459,18 +458,18 @@ struct Complex {
             const uint32_t p4 = pin((abc << 8) | uk);
             pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
         }
-        const uint64_t key = ((uint64_t)dd << 32) | (uint64_t)(~pk);
         // k is a common neighbour iff every distance to it is <= thr (sparse_distance_matrix):
         // the diameter bound covers it, the +inf diagonal excludes k in the simplex, and lanes
         // k >= n (reading past the row) are not vertices
-        return (k < n && dd <= __float_as_uint(thr) && key > floor) ? key : kInf;
+        dd = (k < n && dd <= __float_as_uint(thr)) ? dd : 0xFFFFFFFFu;
+        return ((uint64_t)dd << 32) | (uint64_t)(~pk);
     }
 
-    // lane k's key of the cofacet (V entry e) u {k} above floor (e wave-uniform)
-    __device__ uint64_t entry_key(int dim, int k, int e, uint64_t floor) const {
+    // lane k's key of the cofacet (V entry e) u {k}, minus base (e wave-uniform)
+    __device__ uint64_t entry_key(int dim, int k, int e, uint64_t base) const {
         const uint32_t sx = e < 64 ? rl(vs0, e) : rl(vs1, e - 64);
         const uint32_t dx = e < 64 ? rl(__float_as_uint(vd0), e) : rl(__float_as_uint(vd1), e - 64);
-        return cofacet_key_above(dim, k, sx, __uint_as_float(dx), floor);
+        return cofacet_key(dim, k, sx, dx) - base;
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
@@ -486,27 +485,34 @@ struct Complex {
         if (k < v) vd0 = simplex_diam(dim, vs0);
         if (v > 64 && k + 64 < v) vd1 = simplex_diam(dim, vs1);
         for (;;) {
+            // keys are taken relative to base = floor + 1: key - base wraps the keys <= floor
+            // above every key > floor, so one unsigned minimum skips them (floor is a real key,
+            // never kInf)
+            const uint64_t base = floor + 1;
             uint64_t lmin = kInf;
             // kPvUnroll V entries per step, their distance reads in flight together, then the rest
             int i = 0;
             for (; i + kPvUnroll <= v; i += kPvUnroll) {
                 uint64_t kq[kPvUnroll];
 #pragma unroll
-                for (int u = 0; u < kPvUnroll; ++u) kq[u] = entry_key(dim, k, i + u, floor);
+                for (int u = 0; u < kPvUnroll; ++u) kq[u] = entry_key(dim, k, i + u, base);
 #pragma unroll
                 for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
             }
             for (; i < v; ++i) {
-                const uint64_t key = entry_key(dim, k, i, floor);
+                const uint64_t key = entry_key(dim, k, i, base);
                 lmin = key < lmin ? key : lmin;
             }
-            const uint64_t m = wave_min_u64(lmin);
+            const uint64_t mt = wave_min_u64(lmin);
+            const uint64_t m = mt + base;
 #ifdef DGN_PHASE_TIMING
             ph[24] += 1;
             ph[25] += (uint64_t)v;
 #endif
-            if (m == kInf) return kInf;
-            if (__popcll(ballot(lmin == m)) & 1) return m;
+            // no cofacet above floor: the minimum is a non-neighbour key (high word all ones) or
+            // a wrapped key <= floor
+            if ((uint32_t)(m >> 32) == 0xFFFFFFFFu || m <= floor) return kInf;
+            if (__popcll(ballot(lmin == mt)) & 1) return m;
             floor = m;
         }
     }
@@ -599,6 +605,9 @@ struct Complex {
             uint32_t app = owner >= 0 ? kNone : (have_app ? app0 : apparent_owner_wave(dim, tau));
             DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
+#ifdef DGN_PHASE_TIMING
+            ph[27] += (owner < 0 && app == kNone) ? 1 : 0;  // settled by its initial pivot
+#endif
             if (owner >= 0 || app != kNone) {
                 v_toggle(dim, cp, v);
                 int guard = 0;
@@ -643,6 +652,9 @@ struct Complex {
                     if (owner < 0 && app == kNone) break;  // tau is this column's pivot
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
+#ifdef DGN_PHASE_TIMING
+                ph[28] += tau == kInf ? 1 : 0;
+#endif
                 if (tau == kInf) continue;  // zero column
             }
             // ---- tau is the pivot of this column ----
@@ -704,7 +716,7 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();
-    // +inf diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key_above)
+    // +inf diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key)
     if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0x7F800000u);
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;

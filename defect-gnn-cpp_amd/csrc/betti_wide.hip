@@ -602,7 +602,28 @@ struct WideCx {
             err |= kENA;
             return;
         }
+#ifdef DGN_PHASE_TIMING
+        // diagnostics build: sub-phase cycles of the reduction into phase_cycles[16..21],
+        // pivot-search iterations [24] and their V entries [25], column additions [26]
+        uint64_t sb[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t tq = __builtin_amdgcn_s_memtime();
+        auto sub = [&](int k) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            sb[k] += t - tq;
+            tq = t;
+        };
+#define WSUB(k) sub(k)
+#define WCNT(k, x) (sb[k] += (uint64_t)(x))
+#else
+#define WSUB(k) \
+    do {        \
+    } while (0)
+#define WCNT(k, x) \
+    do {           \
+    } while (0)
+#endif
         sort_na(nna);
+        WSUB(0);
         const uint64_t* K = sp<uint64_t>(ly.na_key);
         const uint64_t* T = sp<uint64_t>(ly.na_tau);
         const uint64_t* V = sp<uint64_t>(ly.na_tv);
@@ -618,7 +639,9 @@ struct WideCx {
             const uint32_t cp = uniw(Cc[ci]);
             const uint32_t birth = (uint32_t)(colkey >> 32);
             uint32_t meta = hfind(tau);
+            WSUB(1);
             uint32_t app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+            WSUB(2);
             int v = 0;  // 0 = lazy: V == {this column}
             if (meta != kNoneW || app != kNoneW) {
                 v_toggle(cp, v);
@@ -641,10 +664,16 @@ struct WideCx {
                         err |= kEWork;
                         break;
                     }
+                    WSUB(3);
+                    WCNT(6, 1);
+                    WCNT(7, v);
                     tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInfW;
+                    WSUB(4);
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
                     meta = hfind(tau);
+                    WSUB(1);
                     app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+                    WSUB(2);
                     if (meta == kNoneW && app == kNoneW) break;  // tau is this column's pivot
                     if (++guard > (1l << 20)) {
                         err |= kEGuard;
@@ -678,8 +707,18 @@ struct WideCx {
                 break;
             }
             ++npiv;
+            WSUB(5);
         }
         __syncthreads();
+#ifdef DGN_PHASE_TIMING
+        if (lane == 0 && bl.phase_cycles) {
+            for (int k = 0; k < 6; ++k) atomicAdd(&bl.phase_cycles[16 + k], (unsigned long long)sb[k]);
+            atomicAdd(&bl.phase_cycles[24], (unsigned long long)sb[6]);
+            atomicAdd(&bl.phase_cycles[25], (unsigned long long)sb[7]);
+        }
+#endif
+#undef WSUB
+#undef WCNT
         // empty the pivot table for the next dimension / complex
         uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint32_t* used = sp<uint32_t>(ly.h_used);

@@ -25,4 +25,7 @@ names = ["load", "prim+edges", "dim1 apparent", "dim1 reduce", "dim2 apparent", 
 tot = sum(ph[:7])
 print(json.dumps({"complexes": A, "s": round(dt, 3), "cycles_per_complex": round(tot / A),
                   "phase_share": {n: round(ph[i] / tot, 4) for i, n in enumerate(names)},
-                  "edges": ph[10] / A, "na1": ph[8] / A, "na2": ph[9] / A}, indent=1))
+                  "edges": ph[10] / A, "na1": ph[8] / A, "na2": ph[9] / A,
+                  "reduce_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(
+                      ["sort", "hfind", "apparent_owner", "toggles", "pivot_of_V", "finalize"])},
+                  "adds_per_complex": ph[24] / A, "mean_V_per_pivot_search": ph[25] / max(ph[24], 1)}, indent=1))
