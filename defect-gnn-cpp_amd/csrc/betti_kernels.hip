@@ -304,27 +304,22 @@ struct Complex {
 
     // F-max facet of pivot tau as (packed vertices)
     __device__ uint32_t max_facet(int dim, uint64_t tau) const {
+        // largest diameter, ties to the smallest index: the facet dropping the largest vertex
+        // first (packed order (b,c) < (a,c) < (a,b), and (b,c,d) < (a,c,d) < (a,b,d) < (a,b,c))
         const uint32_t p = key_packed(tau);
         if (dim == 1) {
             const int a = (p >> 16) & 255, b = (p >> 8) & 255, c = p & 255;
-            uint64_t best = ekey(a, b);
-            int fa = a, fb = b;
-            uint64_t k = ekey(a, c);
-            if (k > best) { best = k; fa = a; fb = c; }
-            k = ekey(b, c);
-            if (k > best) { best = k; fa = b; fb = c; }
-            return pack2(fa, fb);
+            const uint32_t dab = dlowb(a, b), dac = dlowb(a, c), dbc = dlowb(b, c);
+            const uint32_t m = max(max(dab, dac), dbc);
+            return dbc == m ? pack2(b, c) : (dac == m ? pack2(a, c) : pack2(a, b));
         } else {
             const int a = (p >> 24) & 255, b = (p >> 16) & 255, c = (p >> 8) & 255, d = p & 255;
-            uint64_t best = tkey(a, b, c);
-            int fa = a, fb = b, fc = c;
-            uint64_t k = tkey(a, b, d);
-            if (k > best) { best = k; fa = a; fb = b; fc = d; }
-            k = tkey(a, c, d);
-            if (k > best) { best = k; fa = a; fb = c; fc = d; }
-            k = tkey(b, c, d);
-            if (k > best) { best = k; fa = b; fb = c; fc = d; }
-            return pack3(fa, fb, fc);
+            const uint32_t dab = dlowb(a, b), dac = dlowb(a, c), dad = dlowb(a, d);
+            const uint32_t dbc = dlowb(b, c), dbd = dlowb(b, d), dcd = dlowb(c, d);
+            const uint32_t fa = max(max(dbc, dbd), dcd), fb = max(max(dac, dad), dcd);
+            const uint32_t fc = max(max(dab, dad), dbd), fd = max(max(dab, dac), dbc);
+            const uint32_t m = max(max(fa, fb), max(fc, fd));
+            return fa == m ? pack3(b, c, d) : (fb == m ? pack3(a, c, d) : (fc == m ? pack3(a, b, d) : pack3(a, b, c)));
         }
     }
     // Apparent owner of pivot tau (whole wave, uniform): its F-max facet f, if tau is f's
