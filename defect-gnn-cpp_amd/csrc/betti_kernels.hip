@@ -610,8 +610,14 @@ struct Complex {
                     // V ^= V(owner)
                     bool ok = true;
                     if (app != kNone) {
-                        // an apparent owner precedes this column in Ripser's order (key greater)
+                        // an apparent owner precedes this column in Ripser's order (key greater):
+                        // guaranteed (an apparent pair's column is the F-max facet of its pivot),
+                        // verified only in -DDGN_ORDER_CHECK builds (3 distance reads and a
+                        // branch on every apparent addition cost 2.4 % of the Betti pass); the
+                        // parity tests compare every pair with the oracle either way
+#ifdef DGN_ORDER_CHECK
                         if (!(column_key(dim, app) > colkey)) { err |= kErrOrder; return; }
+#endif
                         ok = v_toggle(dim, app, v);
                     } else {
                         const uint32_t m = piv_meta(owner);
