@@ -58,7 +58,7 @@ constexpr uint32_t kErrNA = 1u << 2;
 constexpr uint32_t kErrPiv = 1u << 3;
 constexpr uint32_t kErrPairs = 1u << 4;
 constexpr uint32_t kErrR = 1u << 5;
-constexpr uint32_t kErrOrder = 1u << 6;
+[[maybe_unused]] constexpr uint32_t kErrOrder = 1u << 6;  // -DDGN_ORDER_CHECK builds
 
 // scratch layout per wave (bytes)
 struct ScratchLayout {
