@@ -37,7 +37,10 @@ constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
 constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
 constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
-constexpr int kChunk = 4;         // complexes per dequeue
+#ifndef DGN_CHUNK
+#define DGN_CHUNK 1
+#endif
+constexpr int kChunk = DGN_CHUNK;  // complexes per dequeue (1: the grid drains within one complex; A/B 227.6 vs 230.4 ms at 4)
 #ifndef DGN_PV_UNROLL
 #define DGN_PV_UNROLL 4
 #endif
