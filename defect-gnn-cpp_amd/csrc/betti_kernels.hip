@@ -1256,27 +1256,53 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     }
 }
 
+// device facts for the persistent grids, queried once per device (hipGetDeviceProperties is a
+// slow host call and every Betti call launches up to three grids)
+static int cu_count(int dev) {
+    static int cus[64] = {0};
+    if (dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        hipDeviceProp_t prop;
+        cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    }
+    return cus[dev];
+}
+
 template <int NP>
-static hipError_t launch_np(hipStream_t st, const BettiLaunch& b, int grid_waves, int64_t max_items) {
+static int grid_np(int grid_waves, int64_t max_items) {
     int dev = 0, per_cu = 0;
-    hipError_t e;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    hipDeviceProp_t prop;
-    if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, 0);
-    if (e != hipSuccess || per_cu <= 0) per_cu = 4;
-    int grid = prop.multiProcessorCount * per_cu;
+    (void)hipGetDevice(&dev);
+    static int occ[64] = {0};
+    if (dev >= 0 && dev < 64 && occ[dev] > 0) {
+        per_cu = occ[dev];
+    } else {
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, 0);
+        if (e != hipSuccess || per_cu <= 0) per_cu = 4;
+        if (dev >= 0 && dev < 64) occ[dev] = per_cu;
+    }
+    int grid = cu_count(dev) * per_cu;
     if (grid > grid_waves) grid = grid_waves;
     const int64_t chunks = (max_items + kChunk - 1) / kChunk;
     if (grid > chunks) grid = (int)(chunks > 0 ? chunks : 1);
+    return grid;
+}
+
+static int grid_for(int np, int grid_waves, int64_t max_items) {
+    if (np == 32) return grid_np<32>(grid_waves, max_items);
+    if (np == 48) return grid_np<48>(grid_waves, max_items);
+    return grid_np<64>(grid_waves, max_items);
+}
+
+template <int NP>
+static hipError_t launch_np(hipStream_t st, const BettiLaunch& b, int grid) {
     hipLaunchKernelGGL(betti_kernel<NP>, dim3(grid), dim3(kWave), 0, st, b);
     return hipGetLastError();
 }
 
-static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int grid_waves, int64_t max_items) {
-    if (np == 32) return launch_np<32>(st, b, grid_waves, max_items);
-    if (np == 48) return launch_np<48>(st, b, grid_waves, max_items);
-    return launch_np<64>(st, b, grid_waves, max_items);
+static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int grid) {
+    if (np == 32) return launch_np<32>(st, b, grid);
+    if (np == 48) return launch_np<48>(st, b, grid);
+    return launch_np<64>(st, b, grid);
 }
 
 // Three-level dispatch: the main launch uses the instantiation sized for typical complexes
@@ -1285,7 +1311,7 @@ static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int g
 // betti_wide_kernel (65..512 points). Counters and list lengths live on the device, so nothing
 // synchronizes with the host in between.
 hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
-                        int wide_waves) {
+                        int wide_waves, const BettiFork* fork) {
     const int np_big = np_for(max_points < 64 ? max_points : 64);
     const int np_main = np_big > 48 ? 48 : np_big;
     BettiLaunch m = b;
@@ -1298,15 +1324,34 @@ hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, in
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipError_t e = launch_for(np_main, st, m, grid_waves, b.num_atoms);
+    // scratch slots [0, main_grid) belong to the main launch
+    const int main_grid = grid_for(np_main, fork ? grid_waves - fork->overflow_waves : grid_waves, b.num_atoms);
+    const bool overflow = m.skip_above && np_big > np_main;
+    BettiLaunch o = b;
+    o.work_list = b.overflow_list;
+    o.queue = b.work_counter2;
+    o.skip_above = 0;
+    hipError_t e;
+    if (overflow && fork) {
+        // The few complexes of the overflow tier are the slowest ones: reduced after the main
+        // launch they would add one heavy complex's latency to the pass. Instead they run on a
+        // forked stream beside the main launch, on scratch slots past the main grid's.
+        o.scratch = b.scratch + (int64_t)main_grid * b.scratch_per_wave;
+        const int og = grid_for(np_big, fork->overflow_waves, b.num_atoms);
+        if ((e = hipEventRecord(fork->fork, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(fork->side, fork->fork, 0)) != hipSuccess) return e;
+        if ((e = launch_for(np_big, fork->side, o, og)) != hipSuccess) return e;
+        if ((e = hipEventRecord(fork->join, fork->side)) != hipSuccess) return e;
+    }
+    e = launch_for(np_main, st, m, main_grid);
     if (e != hipSuccess || !m.skip_above) return e;
-    if (np_big > np_main) {
-        BettiLaunch o = b;
-        o.work_list = b.overflow_list;
-        o.queue = b.work_counter2;
-        o.skip_above = 0;
-        e = launch_for(np_big, st, o, grid_waves, b.num_atoms);
-        if (e != hipSuccess) return e;
+    if (overflow) {
+        if (fork) {
+            if ((e = hipStreamWaitEvent(st, fork->join, 0)) != hipSuccess) return e;
+        } else {
+            e = launch_for(np_big, st, o, grid_for(np_big, grid_waves, b.num_atoms));
+            if (e != hipSuccess) return e;
+        }
     }
     if (max_points > 64 && wide) e = launch_betti_wide(st, b, *wide, wide_waves);
     return e;

@@ -91,6 +91,9 @@ struct dgn_ctx {
     // betti workspace
     DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
     int betti_slots = 0;
+    // overflow-tier fork (side stream + events), created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's pivot tables were zeroed for
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
@@ -316,7 +319,15 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         return fail(c, DGN_ERR_UNSUPPORTED,
                     "local complex with " + std::to_string(max_points) + " points exceeds the " +
                         std::to_string(betti_max_points()) + "-point wave64 kernel envelope (see DESIGN.md)");
-    if (c->betti_slots == 0) c->betti_slots = betti_grid_waves(c->device);
+    // scratch slots: the main grid's plus kOverflowWaves for the forked overflow tier
+    constexpr int kOverflowWaves = 512;
+    if (c->betti_slots == 0) c->betti_slots = betti_grid_waves(c->device) + kOverflowWaves;
+    if (!c->side) {
+        HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        HIP_TRY(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+    }
+    const BettiFork fork{c->side, c->ev_fork, c->ev_join, kOverflowWaves};
     const int64_t spw = betti_scratch_bytes_per_wave();
     HIP_TRY(c, c->b_scratch.ensure((size_t)spw * c->betti_slots));
     Scalars* sc = c->scalars.as<Scalars>();
@@ -398,7 +409,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
         HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 5 * sizeof(uint32_t), c->stream));
         TimedLaunch t(c, "betti_vr", bytes, 0.0);
-        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr, wide_waves));
+        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr, wide_waves,
+                                &fork));
         return DGN_OK;
     };
     if (lower) {
@@ -527,6 +539,10 @@ void dgn_ctx_destroy(dgn_ctx* c) {
                       &c->b_disp, &c->b_scratch, &c->b_list, &c->b_lower, &c->b_np, &c->b_w, &c->b_wlist, &c->b_wide,
                       &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
         b->release();
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->host_scalars) (void)hipHostFree(c->host_scalars);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;

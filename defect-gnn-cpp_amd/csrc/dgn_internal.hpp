@@ -124,8 +124,16 @@ hipError_t launch_betti_dist(hipStream_t s, const BettiLaunch& b, const DistLaun
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();
 int betti_grid_waves(int device);
-// main (<= 48 points) + overflow (49..64) + wide (65..512) launches; `wide` null if max_points <= 64
+// side stream for the overflow tier: forked from the launch stream after the bucket pass, joined
+// after the main launch; it owns `overflow_waves` scratch slots past the main grid's
+struct BettiFork {
+    hipStream_t side;
+    hipEvent_t fork, join;
+    int overflow_waves;
+};
+// main (<= 48 points) + overflow (49..64) + wide (65..512) launches; `wide` null if max_points <= 64;
+// `fork` null: the overflow tier runs after the main launch on the same stream
 hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
-                        int wide_waves);
+                        int wide_waves, const BettiFork* fork = nullptr);
 
 }  // namespace dgn
