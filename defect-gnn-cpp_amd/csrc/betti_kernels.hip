@@ -1069,142 +1069,36 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
 }
 
 // ---------------------------------------------------------------------------------------
-// Local distance matrices on the matrix cores (ripser_wrapper.cpp:60-70 + 17-24).
-// One wave per complex: cloud row 0 = pos_i, row k = pos_i + disp_k (betti_features.cpp:67-73)
-// or a caller-given cloud; the K = 3 Gram product as three rank-1 v_mfma_f64_16x16x4_f64
-// (each exactly round(x_ik * x_jk)) summed (p0 + p1) + p2 on the VALU, then
-// sqrt(max(0, (sq_i + sq_j) - 2 dot)) -> f32: bit-identical to the reference's Eigen path.
-// Writes the strict lower triangle in the reference's packing (row i, j < i at i(i-1)/2 + j),
-// the point count and the 1/count(species) weight of each complex.
+// Local distance matrices of caller-given clouds (dgn_host_persistence: compute_persistence,
+// ripser_wrapper.cpp:60-70) on the matrix cores (gram_triangle_*, dgn_device.hpp). One wave per
+// complex. The atom-centred clouds of dgn_*_betti come from betti_dist_search_kernel
+// (graph_kernels.hip), which finds the neighbours itself.
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLaunch dl) {
     __shared__ double sq_s[4][kWideMaxPoints];
     const int lane = lane_id(), w = threadIdx.x >> 6;
     double* sq = sq_s[w];
-    typedef double double4_t __attribute__((ext_vector_type(4)));
     for (int64_t c = (int64_t)blockIdx.x * 4 + w; c < dl.count; c += (int64_t)gridDim.x * 4) {
         const int64_t gi = dl.first + c;
-        int64_t r0 = 0;
-        int n;
-        if (bl.clouds) {
-            n = bl.npoints[gi];
-        } else {
-            r0 = bl.row_ptr[gi];
-            n = (int)(bl.row_ptr[gi + 1] - r0) + 1;
-        }
-        if (lane == 0) dl.npoints[c] = n;
-        // 1/count(species) of the centre's structure (betti_features.cpp:62-63, 77); the structure
-        // comes from the atom -> structure map of the neighbour pass
-        if (bl.species) {
-            int64_t lo;
-            if (bl.atom_struct) {
-                lo = bl.atom_struct[gi];
-            } else {
-                lo = 0;
-                int64_t hi = bl.num_structures - 1;
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi + 1) >> 1;
-                    if (bl.atom_offset[mid] <= gi) lo = mid;
-                    else hi = mid - 1;
-                }
-            }
-            const int64_t s0 = bl.atom_offset[lo], s1 = bl.atom_offset[lo + 1];
-            const int spc = bl.species[gi];
-            int cnt = 0;
-            for (int64_t j = s0 + lane; j < s1; j += kWave) cnt += (bl.species[j] == spc);
-            cnt = wave_sum(cnt);
-            if (lane == 0) dl.weight[c] = 1.0 / (double)cnt;
-        } else if (lane == 0) {
+        const int n = bl.npoints[gi];
+        if (lane == 0) {
+            dl.npoints[c] = n;
             dl.weight[c] = 1.0;
         }
         if (n > kWideMaxPoints) continue;  // the Betti pass flags it
+        const double* cloud = bl.clouds + (int64_t)gi * bl.cloud_stride * 3;
+        float* L = dl.lower + c * bl.tri_stride;
         if (n > 64) {
-            // wide complex: rows read straight from global memory, one 16 x 16 tile at a time
-            const int kq = lane >> 4;
-            auto point = [&](int p, int d) -> double {
-                if (bl.clouds) return bl.clouds[((int64_t)gi * bl.cloud_stride + p) * 3 + d];
-                const double q = bl.pos[3 * gi + d];
-                return p == 0 ? q : q + bl.disp[3 * (r0 + p - 1) + d];
-            };
-            for (int p = lane; p < n; p += kWave) {
-                const double x0 = point(p, 0), x1 = point(p, 1), x2 = point(p, 2);
-                sq[p] = (x0 * x0 + x1 * x1) + x2 * x2;  // rowwise().squaredNorm()
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            float* L = dl.lower + c * bl.tri_stride;
-            const int T = (n + 15) / 16;
-            for (int I = 0; I < T; ++I) {
-                const int ra = 16 * I + (lane & 15);
-                const double xa = (ra < n && kq < 3) ? point(ra, kq) : 0.0;
-                for (int J = 0; J <= I; ++J) {
-                    const int cb = 16 * J + (lane & 15);
-                    const double xb = (cb < n && kq < 3) ? point(cb, kq) : 0.0;
-                    const double4_t z = {0.0, 0.0, 0.0, 0.0};
-                    const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 0 ? xa : 0.0, kq == 0 ? xb : 0.0, z, 0, 0, 0);
-                    const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 1 ? xa : 0.0, kq == 1 ? xb : 0.0, z, 0, 0, 0);
-                    const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 2 ? xa : 0.0, kq == 2 ? xb : 0.0, z, 0, 0, 0);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = 16 * I + (lane >> 4) + 4 * r;
-                        if (row < n && cb < row) {
-                            const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
-                            const double d2 = (sq[row] + sq[cb]) - 2.0 * dot;
-                            L[c2(row) + cb] = (float)sqrt(fmax(d2, 0.0));
-                        }
-                    }
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            gram_triangle_wide(n, sq, L, [&](int p, double x[3]) {
+                x[0] = cloud[3 * p];
+                x[1] = cloud[3 * p + 1];
+                x[2] = cloud[3 * p + 2];
+            });
             continue;
         }
-        // lane p holds cloud row p; all loads issued together
         const int pl = lane < n ? lane : n - 1;
-        double px[3];
-        if (bl.clouds) {
-            const double* xc = bl.clouds + ((int64_t)gi * bl.cloud_stride + pl) * 3;
-            px[0] = xc[0]; px[1] = xc[1]; px[2] = xc[2];
-        } else {
-            const double* q = bl.pos + 3 * gi;
-            const double* dv = bl.disp + 3 * (r0 + (pl > 0 ? pl - 1 : 0));
-            const double d0v = dv[0], d1v = dv[1], d2v = dv[2];
-            px[0] = pl == 0 ? q[0] : q[0] + d0v;
-            px[1] = pl == 0 ? q[1] : q[1] + d1v;
-            px[2] = pl == 0 ? q[2] : q[2] + d2v;
-        }
-        sq[lane] = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
-        const int T = (n + 15) / 16;
-        const int kk = lane >> 4;
-        double xr[4];  // coordinate kk of cloud row 16 I + (lane & 15)
-#pragma unroll
-        for (int I = 0; I < 4; ++I) {
-            const int ra = 16 * I + (lane & 15);
-            const double v0 = __shfl(px[0], ra, kWave), v1 = __shfl(px[1], ra, kWave), v2 = __shfl(px[2], ra, kWave);
-            xr[I] = (ra < n && kk < 3) ? (kk == 0 ? v0 : (kk == 1 ? v1 : v2)) : 0.0;
-        }
-        float* L = dl.lower + c * bl.tri_stride;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        for (int I = 0; I < T; ++I) {
-            for (int J = 0; J <= I; ++J) {
-                const double xa = I == 0 ? xr[0] : (I == 1 ? xr[1] : (I == 2 ? xr[2] : xr[3]));
-                const double xb = J == 0 ? xr[0] : (J == 1 ? xr[1] : (J == 2 ? xr[2] : xr[3]));
-                const double4_t z = {0.0, 0.0, 0.0, 0.0};
-                // rank-1 products: operand k' nonzero only for k' == k -> round(x_ik * x_jk)
-                const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 0 ? xa : 0.0, kk == 0 ? xb : 0.0, z, 0, 0, 0);
-                const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 1 ? xa : 0.0, kk == 1 ? xb : 0.0, z, 0, 0, 0);
-                const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 2 ? xa : 0.0, kk == 2 ? xb : 0.0, z, 0, 0, 0);
-                const int col = 16 * J + (lane & 15);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = 16 * I + (lane >> 4) + 4 * r;
-                    if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
-                        const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
-                        const double d2 = (sq[row] + sq[col]) - 2.0 * dot;
-                        L[c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const double px[3] = {cloud[3 * pl], cloud[3 * pl + 1], cloud[3 * pl + 2]};
+        gram_triangle_narrow(px, n, sq, L);
     }
 }
 
@@ -1219,6 +1113,12 @@ hipError_t launch_betti_dist(hipStream_t st, const BettiLaunch& b, const DistLau
 // ---------------------------------------------------------------------------------------
 int betti_max_points() { return kWideMaxPoints; }
 int64_t betti_scratch_bytes_per_wave() { return ScratchLayout::total; }
+
+hipError_t betti_init_scratch(hipStream_t s, uint8_t* base, int slots) {
+    // the triangle table and the edge table are adjacent: one 2D memset over all slots
+    const size_t width = (size_t)(ScratchLayout::mincof_e + 64 * 63 / 2 - ScratchLayout::mincof);
+    return hipMemset2DAsync(base + ScratchLayout::mincof, (size_t)ScratchLayout::total, kMcNone, width, (size_t)slots, s);
+}
 
 static int np_for(int max_points) { return max_points <= 32 ? 32 : (max_points <= 48 ? 48 : 64); }
 

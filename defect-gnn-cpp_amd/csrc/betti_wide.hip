@@ -886,6 +886,13 @@ WideLayout betti_wide_layout(int nmax) {
     return l;
 }
 
+hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves) {
+    hipError_t e = hipMemset2DAsync(l.base + l.h_key, (size_t)l.total, 0, 8 * (size_t)l.h_cap, (size_t)waves, s);
+    if (e != hipSuccess) return e;
+    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges
+    return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
+}
+
 // waves of betti_wide_kernel resident on the whole device for complexes of up to nmax points
 int betti_wide_resident_waves(int device, int nmax) {
     hipDeviceProp_t prop;

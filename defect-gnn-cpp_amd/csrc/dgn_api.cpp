@@ -22,6 +22,10 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
     hipError_t ensure(size_t want) {
         if (want <= bytes && p) return hipSuccess;
         if (p) (void)hipFree(p);
@@ -59,13 +63,35 @@ struct Scalars {  // device-side scalars, one allocation
     int64_t total;
     unsigned long long sum_sq;  // sum over atoms of (candidates + 1)^2
     uint32_t max_candidates;
-    uint32_t error_flag;
-    uint32_t work_counter;   // betti main launch queue
-    uint32_t work_counter2;  // betti overflow launch queue
-    uint32_t overflow_len;   // complexes routed to the overflow launch
-    uint32_t wide_queue;     // betti wide launch queue
-    uint32_t wide_len;       // complexes routed to the wide launch
+    uint32_t max_natoms;        // largest structure of the batch (prep)
+    uint32_t graph_flag;        // graph error bits kGErr* (prep, emit, Betti search)
+    uint32_t error_flag;        // Betti reduction error bits
+    uint32_t work_counter;      // betti main launch queue
+    uint32_t work_counter2;     // betti overflow launch queue
+    uint32_t overflow_len;      // complexes routed to the overflow launch
+    uint32_t wide_queue;        // betti wide launch queue
+    uint32_t wide_len;          // complexes routed to the wide launch
     uint32_t pad[1];
+};
+
+// one neighbour pass's device workspace and the facts its count recorded (count -> emit handshake)
+struct GraphWork {
+    DevBuf meta, counts, block_sums, block_aux, atom_struct, cell_start, cell_pos, mask, weight;
+    bool have = false;
+    const double* pos = nullptr;
+    int64_t atoms = -1, structs = -1;
+    double rc = 0, eps = 0;
+    uint64_t k = 0;
+    uint32_t max_candidates = 0, max_natoms = 0;
+    int64_t edges = 0;
+    double sum_sq = 0;
+};
+
+// host-pinned mirror: the scalars after a count pass, and the emit's deferred error flag
+struct HostScalars {
+    Scalars s;
+    uint32_t emit_flag;  // copied asynchronously after every graph emit
+    uint32_t pad;
 };
 
 }  // namespace
@@ -75,26 +101,21 @@ struct dgn_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     std::string last_error;
-    // graph workspace
-    DevBuf meta, counts, block_sums, block_aux, atom_struct, rows_d, rows_j, scalars;
-    bool cnt_rows = false;  // the count pass stored ranked rows (streaming emit path)
-    Scalars* host_scalars = nullptr;  // pinned
-    // count->emit handshake
-    bool have_count = false;
-    const double* cnt_pos = nullptr;
-    int64_t cnt_atoms = -1, cnt_structs = -1;
-    double cnt_rc = 0, cnt_eps = 0;
-    uint64_t cnt_k = 0;
-    uint32_t cnt_max_candidates = 0;
-    int64_t cnt_edges = 0;
-    double cnt_sum_sq = 0;
+    // neighbour-pass workspaces: `gw` for dgn_dev_graph_count -> dgn_dev_graph_emit, `bw` for the
+    // Betti pass's own NeighborList(rc, SIZE_MAX) (so a Betti call between a graph count and its
+    // emit does not disturb the handshake)
+    GraphWork gw, bw;
+    DevBuf scalars;
+    HostScalars* host = nullptr;  // pinned
+    bool emit_pending = false;    // an emit's error flag is on its way to host->emit_flag
     // betti workspace
-    DevBuf b_row_ptr, b_col, b_dist, b_disp, b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
+    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
     int betti_slots = 0;
+    bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's pivot tables were zeroed for
+    int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's tables were initialised for
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
 #ifdef DGN_PHASE_TIMING
@@ -177,7 +198,7 @@ bool batch_ok(const dgn_batch* b) {
 }
 
 RbfSpec make_rbf(const dgn_graph_params* p) {
-    RbfSpec r;
+    RbfSpec r{};
     r.dtype = p->rbf_dtype;
     r.nbins = dgn_rbf_bins(p->rbf_cutoff, p->rbf_dr);
     r.dr = p->rbf_dr;
@@ -185,112 +206,130 @@ RbfSpec make_rbf(const dgn_graph_params* p) {
     const double sigma = p->rbf_cutoff / 3;
     r.inv_sigma2 = 1 / std::pow(sigma, 2);
     r.norm = 1 / (sigma * std::sqrt(2 * M_PI));
+    r.c2 = -0.5 * r.inv_sigma2 * 1.4426950408889634074;  // exponent scale of the f32 path (log2 e)
     r.inv_nbins = r.nbins > 0 ? 1.0f / (float)r.nbins : 0.0f;
     r.norm_f = (float)r.norm;
     return r;
 }
 
-// graph counting pass shared by the graph and Betti entry points
-// `betti` = the neighbour pass internal to dgn_*_betti (timed under its own names so the graph
-// kernels' roofline is never mixed with it)
+// A graph emit reports its consistency flag asynchronously (host->emit_flag); the next call
+// that synchronizes the stream surfaces it.
+int take_emit_flag(dgn_ctx* c) {
+    if (!c->emit_pending) return DGN_OK;
+    c->emit_pending = false;
+    const uint32_t f = c->host->emit_flag;
+    if (f & kGErrCap) return fail(c, DGN_ERR_INTERNAL, "graph emit: more candidates than the count pass reported");
+    if (f) return fail(c, DGN_ERR_INTERNAL, "graph emit disagreed with the count pass (flags " + std::to_string(f) + ")");
+    return DGN_OK;
+}
+
+GraphLaunch graph_launch(GraphWork& W, const dgn_batch* b, double rc, double eps, uint64_t kmax, bool use_mask) {
+    return GraphLaunch{W.meta.as<StructMeta>(),  W.atom_struct.as<int32_t>(),
+                       b->atom_offset,           b->positions,
+                       W.cell_start.as<int32_t>(), W.cell_pos.as<double4>(),
+                       use_mask ? W.mask.as<uint64_t>() : nullptr,
+                       b->num_structures,        b->num_atoms,
+                       rc * rc,                  eps,
+                       kmax};
+}
+
+// neighbour counting pass shared by the graph and Betti entry points: prep (geometry, atom map,
+// cell lists, Betti weights) + per-atom counts and exact hit masks + block scan; one stream
+// synchronization. `betti` = the neighbour pass internal to dgn_*_betti (its own workspace, timed
+// under its own names so the graph kernels' roofline is never mixed with it; also computes the
+// per-atom 1/count(species) weight)
 int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, double eps, int64_t* num_edges,
                      bool betti = false) {
+    GraphWork& W = betti ? c->bw : c->gw;
     const int64_t A = b->num_atoms, B = b->num_structures;
     const int64_t nblocks = graph_blocks(A);
-    HIP_TRY(c, c->meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
-    HIP_TRY(c, c->counts.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
-    HIP_TRY(c, c->block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
-    HIP_TRY(c, c->block_aux.ensure(2 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
-    HIP_TRY(c, c->atom_struct.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(A, 1)));
+    const size_t A1 = (size_t)std::max<int64_t>(A, 1);
+    HIP_TRY(c, W.meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
+    HIP_TRY(c, W.counts.ensure(sizeof(int32_t) * A1));
+    HIP_TRY(c, W.block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, W.block_aux.ensure(3 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, W.atom_struct.ensure(sizeof(int32_t) * A1));
+    HIP_TRY(c, W.cell_start.ensure(sizeof(int32_t) * (size_t)(A + B + 1)));
+    HIP_TRY(c, W.cell_pos.ensure(sizeof(double4) * A1));
+    HIP_TRY(c, W.mask.ensure(sizeof(uint64_t) * kMaskWords * A1));
+    const bool want_weight = betti && b->species;
+    if (want_weight) HIP_TRY(c, W.weight.ensure(sizeof(double) * A1));
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(sc, 0, sizeof(Scalars), c->stream));
+    W.have = false;
     {
-        TimedLaunch t(c, betti ? "betti_nl_prep" : "prep_structures", (double)B * (72 + 16), 0);
-        HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, B, rc, c->meta.as<StructMeta>(),
-                                          c->atom_struct.as<int32_t>()));
+        TimedLaunch t(c, betti ? "betti_nl_prep" : "prep_structures", (double)B * (72 + 16 + sizeof(StructMeta)) + 4.0 * A, 0);
+        HIP_TRY(c, launch_prep_structures(c->stream, b->lattice, b->atom_offset, b->positions,
+                                          want_weight ? b->species : nullptr, B, rc, W.meta.as<StructMeta>(),
+                                          W.atom_struct.as<int32_t>(), W.cell_start.as<int32_t>(),
+                                          W.cell_pos.as<double4>(), want_weight ? W.weight.as<double>() : nullptr,
+                                          &sc->graph_flag));
     }
-    GraphLaunch g{c->meta.as<StructMeta>(), c->atom_struct.as<int32_t>(), b->atom_offset, b->positions, B, A,
-                  rc * rc, eps, kmax};
-    // stored-rows path: the count pass ranks and keeps each atom's rows, the emit pass streams
-    const bool rows = !betti && kmax > 0 && kmax <= (uint64_t)kRowsMaxK && A > 0;
-    if (rows) {
-        HIP_TRY(c, c->rows_d.ensure(sizeof(uint64_t) * (size_t)A * (size_t)kmax));
-        HIP_TRY(c, c->rows_j.ensure(sizeof(uint64_t) * (size_t)A * (size_t)kmax));
-    }
+    const GraphLaunch g = graph_launch(W, b, rc, eps, kmax, false);
     {
-        TimedLaunch t(c, betti ? "betti_nl_count" : "graph_count", (double)A * (24 + 4), 0);
-        HIP_TRY(c, launch_graph_count(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
-                                      c->block_aux.as<uint64_t>(), rows ? c->rows_d.as<uint64_t>() : nullptr,
-                                      rows ? c->rows_j.as<uint64_t>() : nullptr));
+        // compulsory traffic: positions in, per-atom counts out (+ the structure metadata)
+        TimedLaunch t(c, betti ? "betti_nl_count" : "graph_count", (double)A * (24 + 4) + (double)B * sizeof(StructMeta), 0);
+        HIP_TRY(c, launch_graph_count(c->stream, g, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
+                                      W.block_aux.as<uint64_t>(), W.mask.as<uint64_t>()));
     }
     {
-        TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 16, 0);
-        HIP_TRY(c, launch_block_scan(c->stream, c->block_sums.as<int64_t>(), c->block_aux.as<uint64_t>(), nblocks,
-                                     &sc->total, &sc->max_candidates, &sc->sum_sq));
+        TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 32, 0);
+        HIP_TRY(c, launch_block_scan(c->stream, W.block_sums.as<int64_t>(), W.block_aux.as<uint64_t>(), nblocks,
+                                     &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms));
     }
-    HIP_TRY(c, hipMemcpyAsync(c->host_scalars, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(&c->host->s, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    c->have_count = true;
-    c->cnt_pos = b->positions;
-    c->cnt_atoms = A;
-    c->cnt_structs = B;
-    c->cnt_rc = rc;
-    c->cnt_eps = eps;
-    c->cnt_k = kmax;
-    c->cnt_max_candidates = c->host_scalars->max_candidates;
-    c->cnt_edges = c->host_scalars->total;
-    c->cnt_sum_sq = (double)c->host_scalars->sum_sq;
-    c->cnt_rows = rows && c->cnt_max_candidates <= (uint32_t)kRowsCap;
-    if (num_edges) *num_edges = c->cnt_edges;
+    int st = take_emit_flag(c);
+    if (st) return st;
+    if (c->host->s.graph_flag & kGErrFar)
+        return fail(c, DGN_ERR_UNSUPPORTED, "an atom lies more than 500 lattice periods from the origin");
+    W.have = true;
+    W.pos = b->positions;
+    W.atoms = A;
+    W.structs = B;
+    W.rc = rc;
+    W.eps = eps;
+    W.k = kmax;
+    W.max_candidates = c->host->s.max_candidates;
+    W.max_natoms = c->host->s.max_natoms;
+    W.edges = c->host->s.total;
+    W.sum_sq = (double)c->host->s.sum_sq;
+    if (num_edges) *num_edges = W.edges;
     return DGN_OK;
 }
 
 int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int32_t* col, double* dist,
-                    double* disp, void* rbf, const RbfSpec& rs, bool betti = false) {
-    if (!c->have_count || c->cnt_pos != b->positions || c->cnt_atoms != b->num_atoms)
+                    double* disp, void* rbf, const RbfSpec& rs) {
+    GraphWork& W = c->gw;
+    if (!W.have || W.pos != b->positions || W.atoms != b->num_atoms)
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
-    const int cap = graph_emit_cap(c->cnt_max_candidates);
+    const int cap = graph_emit_cap(W.max_candidates);
     if (cap == 0)
         return fail(c, DGN_ERR_UNSUPPORTED, "more than 512 neighbour candidates for one atom (cutoff too large)");
     if (b->num_atoms == 0) return DGN_OK;
     Scalars* sc = c->scalars.as<Scalars>();
-    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, sizeof(uint32_t), c->stream));
-    GraphLaunch g{c->meta.as<StructMeta>(), c->atom_struct.as<int32_t>(), b->atom_offset, b->positions,
-                  c->cnt_structs, c->cnt_atoms,
-                  c->cnt_rc * c->cnt_rc, c->cnt_eps, c->cnt_k};
-    const double E = (double)c->cnt_edges, A = (double)c->cnt_atoms;
+    HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, sizeof(uint32_t), c->stream));
+    const GraphLaunch g = graph_launch(W, b, W.rc, W.eps, W.k, true);
+    const double E = (double)W.edges, A = (double)W.atoms, B = (double)W.structs;
     const double rbf_bytes = rs.dtype == DGN_F32 ? 4.0 : (rs.dtype == DGN_F64 ? 8.0 : 0.0);
-    const double out_bytes = 8 * (A + 1) + E * (4 + (dist ? 8 : 0)) + (disp ? 24 * E : 0) +
-                             (rbf ? E * rs.nbins * rbf_bytes : 0);
-    if (c->cnt_rows) {
-        // compulsory traffic of the streaming emit: counts + stored rows in, CSR + features out
-        // (+ both endpoint positions for displacements)
-        const double bytes = 4 * A + 16 * E + out_bytes + (disp ? 48 * E : 0);
-        TimedLaunch t(c, betti ? "betti_nl_emit" : "graph_emit", bytes, 0);
-        HIP_TRY(c, launch_graph_emit_rows(c->stream, g, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
-                                          c->rows_d.as<uint64_t>(), c->rows_j.as<uint64_t>(),
-                                          const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs));
-        return DGN_OK;
-    }
-    // recompute path: positions + lattice in, counts in, CSR + features out
-    const double bytes = A * 24 + (double)c->cnt_structs * 72 + 4 * A + out_bytes;
+    // compulsory traffic: positions + lattice + counts in; CSR + edge features out
+    const double bytes = 24 * A + 72 * B + 4 * A + 8 * (A + 1) + E * (4 + (dist ? 8 : 0)) + (disp ? 24 * E : 0) +
+                         (rbf ? E * rs.nbins * rbf_bytes : 0);
+    const int stage = (int)std::min<uint32_t>(W.max_natoms, (uint32_t)kStage);
     {
-        TimedLaunch t(c, betti ? "betti_nl_emit" : "graph_emit", bytes, 0);
-        HIP_TRY(c, launch_graph_emit(c->stream, g, cap, c->counts.as<int32_t>(), c->block_sums.as<int64_t>(),
-                                     const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs, &sc->error_flag));
+        TimedLaunch t(c, "graph_emit", bytes, 0);
+        HIP_TRY(c, launch_graph_emit(c->stream, g, cap, stage, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
+                                     const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs, &sc->graph_flag));
     }
+    HIP_TRY(c, hipMemcpyAsync(&c->host->emit_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    c->emit_pending = true;
     return DGN_OK;
 }
 
 int check_emit_flag(dgn_ctx* c) {
-    Scalars* sc = c->scalars.as<Scalars>();
-    HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (c->host_scalars->error_flag)
-        return fail(c, DGN_ERR_INTERNAL, "graph emit consistency flag " + std::to_string(c->host_scalars->error_flag));
-    return DGN_OK;
+    return take_emit_flag(c);
 }
 
 int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int32_t* counts, const double* clouds,
@@ -301,24 +340,17 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     if (A == 0) return DGN_OK;
     int max_points = cloud_stride;
     if (!given) {
+        // NeighborList(rc, SIZE_MAX) counts (betti_features.cpp:107): the largest local complex,
+        // sum n^2 for the byte accounting, the per-atom weights
         int64_t E = 0;
         int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E, true);
         if (st) return st;
-        HIP_TRY(c, c->b_row_ptr.ensure(sizeof(int64_t) * (size_t)(A + 1)));
-        HIP_TRY(c, c->b_col.ensure(sizeof(int32_t) * (size_t)std::max<int64_t>(E, 1)));
-        HIP_TRY(c, c->b_dist.ensure(sizeof(double) * (size_t)std::max<int64_t>(E, 1)));
-        HIP_TRY(c, c->b_disp.ensure(sizeof(double) * 3 * (size_t)std::max<int64_t>(E, 1)));
-        RbfSpec none{};
-        none.dtype = DGN_NONE;
-        st = graph_emit_impl(c, b, c->b_row_ptr.as<int64_t>(), c->b_col.as<int32_t>(), c->b_dist.as<double>(),
-                             c->b_disp.as<double>(), nullptr, none, true);
-        if (st) return st;
-        max_points = (int)c->cnt_max_candidates + 1;
+        max_points = (int)c->bw.max_candidates + 1;
     }
     if (max_points > betti_max_points())
         return fail(c, DGN_ERR_UNSUPPORTED,
                     "local complex with " + std::to_string(max_points) + " points exceeds the " +
-                        std::to_string(betti_max_points()) + "-point wave64 kernel envelope (see DESIGN.md)");
+                        std::to_string(betti_max_points()) + "-point kernel envelope (see DESIGN.md)");
     // scratch slots: the main grid's plus kOverflowWaves for the forked overflow tier
     constexpr int kOverflowWaves = 512;
     if (c->betti_slots == 0) c->betti_slots = betti_grid_waves(c->device) + kOverflowWaves;
@@ -329,11 +361,19 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     }
     const BettiFork fork{c->side, c->ev_fork, c->ev_join, kOverflowWaves};
     const int64_t spw = betti_scratch_bytes_per_wave();
-    HIP_TRY(c, c->b_scratch.ensure((size_t)spw * c->betti_slots));
-    Scalars* sc = c->scalars.as<Scalars>();
+    if (c->b_scratch.bytes < (size_t)spw * c->betti_slots) {
+        HIP_TRY(c, c->b_scratch.ensure((size_t)spw * c->betti_slots));
+        c->scratch_fresh = true;
+    }
+    if (c->scratch_fresh) {
+        // every slot's one-byte min-cofacet tables start as "no cofacet" (0xFF): the kernels keep
+        // that invariant for every entry they touch, so a stray byte can never read as a clearing mark
+        HIP_TRY(c, betti_init_scratch(c->stream, c->b_scratch.as<uint8_t>(), c->betti_slots));
+        c->scratch_fresh = false;
+    }
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
-    sc = c->scalars.as<Scalars>();
-    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, 4 * sizeof(uint32_t), c->stream));
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, 5 * sizeof(uint32_t), c->stream));
     HIP_TRY(c, c->b_list.ensure(sizeof(int32_t) * (size_t)A));
     // complexes above 64 points: the wide kernel, one wave per complex with a per-wave scratch
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
@@ -354,23 +394,16 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
         if (grown || c->wide_nmax != max_points || c->wide_waves != wide_waves) {
-            // the layout depends on max_points: every wave's pivot hash table starts empty (key 0);
-            // afterwards each reduction empties the slots it used
-            HIP_TRY(c, hipMemset2DAsync(wl.base + wl.h_key, (size_t)wl.total, 0, 8 * (size_t)wl.h_cap,
-                                        (size_t)wide_waves, c->stream));
+            // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
+            // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
+            // restores both for the entries it used
+            HIP_TRY(c, betti_wide_init_scratch(c->stream, wl, wide_waves));
             c->wide_nmax = max_points;
             c->wide_waves = wide_waves;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
     BettiLaunch bl{};
-    bl.row_ptr = given ? nullptr : c->b_row_ptr.as<int64_t>();
-    bl.disp = given ? nullptr : c->b_disp.as<double>();
-    bl.pos = given ? nullptr : b->positions;
-    bl.species = given ? nullptr : b->species;
-    bl.atom_offset = given ? nullptr : b->atom_offset;
-    bl.atom_struct = given ? nullptr : c->atom_struct.as<int32_t>();  // written by graph_count_impl
-    bl.num_structures = given ? 0 : b->num_structures;
     bl.num_atoms = A;
     bl.thr = (float)rc;  // ripser_wrapper.cpp:28
     bl.features = features;
@@ -413,6 +446,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                                 &fork));
         return DGN_OK;
     };
+    // triangles: floats per complex, padded to a multiple of 4 (16-byte aligned complexes)
+    const int64_t tri_stride = std::max<int64_t>(4, ((int64_t)max_points * (max_points - 1) / 2 + 3) / 4 * 4);
     if (lower) {
         // caller-given triangles: the Betti pass alone
         int st = vr_pass(0, A, lower, (int64_t)cloud_stride * (cloud_stride - 1) / 2, npoints, nullptr, 0.0);
@@ -420,40 +455,51 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     } else {
         // distance pass (MFMA) + Betti pass per chunk of complexes; the triangle buffer is
         // bounded (~16 GB of the 288 GB HBM) so arbitrarily large shards stream through it
-        // floats per complex, padded to a multiple of 4 (16-byte aligned complexes)
-        const int64_t tri_stride = std::max<int64_t>(4, ((int64_t)max_points * (max_points - 1) / 2 + 3) / 4 * 4);
         const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(16) << 30) / (4 * tri_stride)));
-        bl.tri_stride = tri_stride;  // the distance pass writes [chunk][tri_stride]
         HIP_TRY(c, c->b_lower.ensure(sizeof(float) * (size_t)(chunk * tri_stride)));
         HIP_TRY(c, c->b_np.ensure(sizeof(int32_t) * (size_t)chunk));
         HIP_TRY(c, c->b_w.ensure(sizeof(double) * (size_t)chunk));
         // per-complex averages over the batch: points n (sum n = E + A), sum n^2 from the count pass
-        const double En = given ? 0.0 : (double)c->cnt_edges, An = (double)A;
-        const double sum_n2 = given ? 0.0 : c->cnt_sum_sq;
+        const double En = given ? 0.0 : (double)c->bw.edges, An = (double)A;
+        const double sum_n2 = given ? 0.0 : c->bw.sum_sq;
+        const GraphLaunch g = given ? GraphLaunch{} : graph_launch(c->bw, b, rc, 1e-10, UINT64_MAX, true);
         for (int64_t c0 = 0; c0 < A; c0 += chunk) {
             const int64_t cnt = std::min<int64_t>(chunk, A - c0);
             const double f = (double)cnt / An;
-            DistLaunch dl{c0, cnt, c->b_lower.as<float>(), c->b_np.as<int32_t>(), c->b_w.as<double>()};
             {
-                // algorithmic bytes: displacements + row_ptr + centre position in, triangles (4 C(n,2))
-                // + point count + weight out; useful flops 6 n^2 per complex
-                const double bytes = given ? 0.0 : f * (24 * En + 8 * An + 24 * An + 2 * (sum_n2 - (En + An)) + 12 * An);
+                // algorithmic bytes: the structures' positions in, triangles (4 C(n,2)) + point count
+                // out; useful flops 6 n^2 per complex
+                const double bytes = given ? 0.0 : f * (24 * An + 2 * (sum_n2 - (En + An)) + 4 * An);
                 TimedLaunch t(c, "betti_dist", bytes, given ? 0.0 : f * 6.0 * sum_n2);
-                HIP_TRY(c, launch_betti_dist(c->stream, bl, dl));
+                if (given) {
+                    BettiLaunch db = bl;
+                    db.tri_stride = tri_stride;
+                    DistLaunch dl{c0, cnt, c->b_lower.as<float>(), c->b_np.as<int32_t>(), c->b_w.as<double>()};
+                    HIP_TRY(c, launch_betti_dist(c->stream, db, dl));
+                } else {
+                    HIP_TRY(c, launch_betti_dist_search(c->stream, g, c0, cnt, max_points, tri_stride,
+                                                        c->bw.counts.as<int32_t>(), c->b_lower.as<float>(),
+                                                        c->b_np.as<int32_t>(), &sc->graph_flag));
+                }
             }
             // Betti pass: triangles in, 35 f64 + 4 i32 out
             const double bytes = given ? 0.0 : f * (2 * (sum_n2 - (En + An)) + 12 * An + An * (35 * 8 + 16));
-            int st = vr_pass(c0, cnt, c->b_lower.as<float>(), tri_stride, c->b_np.as<int32_t>(), c->b_w.as<double>(), bytes);
+            const double* w = given ? c->b_w.as<double>() : (b->species ? c->bw.weight.as<double>() + c0 : nullptr);
+            int st = vr_pass(c0, cnt, c->b_lower.as<float>(), tri_stride, c->b_np.as<int32_t>(), w, bytes);
             if (st) return st;
         }
     }
-    HIP_TRY(c, hipMemcpyAsync(&c->host_scalars->error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+    HIP_TRY(c, hipMemcpyAsync(&c->host->s.graph_flag, &sc->graph_flag, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                               c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, hipMemcpy(c->phase_host, c->phase.p, sizeof(c->phase_host), hipMemcpyDeviceToHost));
 #endif
-    const uint32_t f = c->host_scalars->error_flag;
+    if (int st = take_emit_flag(c)) return st;
+    if (c->host->s.graph_flag)
+        return fail(c, DGN_ERR_INTERNAL,
+                    "Betti neighbour search disagreed with the count pass (flags " + std::to_string(c->host->s.graph_flag) + ")");
+    const uint32_t f = c->host->s.error_flag;
     if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
     if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
     if (f) return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
@@ -515,16 +561,19 @@ int dgn_ctx_create(int device, dgn_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return DGN_ERR_HIP;
     dgn_ctx* c = new dgn_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    // a blocking stream: ordered after (and before) the legacy null stream, which is where a
+    // caller's default-stream work (torch's default stream reports handle 0) runs
+    if (hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess) {
         delete c;
         return DGN_ERR_HIP;
     }
     c->stream = c->own;
-    if (hipHostMalloc((void**)&c->host_scalars, sizeof(Scalars), hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&c->host, sizeof(HostScalars), hipHostMallocDefault) != hipSuccess) {
         (void)hipStreamDestroy(c->own);
         delete c;
         return DGN_ERR_HIP;
     }
+    std::memset(c->host, 0, sizeof(HostScalars));
     *out = c;
     return DGN_OK;
 }
@@ -533,23 +582,21 @@ void dgn_ctx_destroy(dgn_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     fold_events(c);
     for (hipEvent_t e : c->free_events) (void)hipEventDestroy(e);
-    for (DevBuf* b : {&c->meta, &c->counts, &c->block_sums, &c->block_aux, &c->atom_struct, &c->rows_d, &c->rows_j, &c->scalars, &c->b_row_ptr, &c->b_col, &c->b_dist,
-                      &c->b_disp, &c->b_scratch, &c->b_list, &c->b_lower, &c->b_np, &c->b_w, &c->b_wlist, &c->b_wide,
-                      &c->h_lat, &c->h_pos, &c->h_spec, &c->h_off})
-        b->release();
-    if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->host_scalars) (void)hipHostFree(c->host_scalars);
+    if (c->host) (void)hipHostFree(c->host);
     if (c->own) (void)hipStreamDestroy(c->own);
-    delete c;
+    delete c;  // DevBuf destructors free the device workspaces
 }
 
 int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
     if (!c) return DGN_ERR_ARG;
+    // NULL (the legacy null stream, e.g. torch's default stream) -> the context's own blocking
+    // stream, which the null stream orders against; anything else is used as given
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
     return DGN_OK;
 }
@@ -557,7 +604,7 @@ int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
 int dgn_ctx_synchronize(dgn_ctx* c) {
     if (!c) return DGN_ERR_ARG;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return DGN_OK;
+    return take_emit_flag(c);  // a pending graph-emit consistency failure surfaces here
 }
 
 const char* dgn_ctx_last_error(const dgn_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
@@ -620,7 +667,7 @@ int dgn_dev_graph_count(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* 
 int dgn_dev_graph_emit(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* p, int64_t* row_ptr,
                        const dgn_graph_out* o) {
     if (!c || !p || !batch_ok(b) || !o || !row_ptr || !o->col_idx) return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: bad args");
-    if (p->r_cutoff != c->cnt_rc || p->max_neighbors != c->cnt_k || p->epsilon != c->cnt_eps)
+    if (p->r_cutoff != c->gw.rc || p->max_neighbors != c->gw.k || p->epsilon != c->gw.eps)
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: parameters differ from the count pass");
     if (p->rbf_dtype != DGN_NONE && (!(p->rbf_dr > 0) || dgn_rbf_bins(p->rbf_cutoff, p->rbf_dr) <= 0))
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: bad RBF parameters");
@@ -717,6 +764,10 @@ int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, do
     hipError_t e;
     if ((e = f.ensure(8 * 35 * std::max<int64_t>(A, 1))) || (e = k.ensure(16 * std::max<int64_t>(A, 1))))
         return hip_fail(c, e, "dgn_host_betti: allocation");
+    // NaN features / -1 counts unless a kernel writes them (a call rejected before any launch
+    // returns those rather than uninitialised device memory)
+    HIP_TRY(c, hipMemsetAsync(f.p, 0xFF, 8 * 35 * (size_t)A, c->stream));
+    HIP_TRY(c, hipMemsetAsync(k.p, 0xFF, 16 * (size_t)A, c->stream));
     st = dgn_dev_betti(c, &d, p, f.as<double>(), k.as<int32_t>());
     if (st == DGN_OK || st == DGN_ERR_CAPACITY || st == DGN_ERR_UNSUPPORTED) {
         if (A) {
@@ -725,8 +776,6 @@ int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, do
             if (e) st = hip_fail(c, e, "dgn_host_betti: copy back");
         }
     }
-    f.release();
-    k.release();
     return st;
 }
 
@@ -766,10 +815,6 @@ static int host_persistence_common(dgn_ctx* c, const double* clouds, const float
         for (int64_t i = 0; i < C; ++i)
             if (kk[4 * i] > cap || kk[4 * i + 2] > cap || kk[4 * i + 3] > cap) st = fail(c, DGN_ERR_CAPACITY, "pair cap");
     }
-    dc.release();
-    dn.release();
-    dp.release();
-    dk.release();
     return st;
 }
 
@@ -810,8 +855,6 @@ int dgn_host_rbf(dgn_ctx* c, const double* distances, int64_t E, double rbf_cuto
     }
     HIP_TRY(c, hipMemcpyAsync(out, dout.p, elem * (size_t)E * rs.nbins, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    dd.release();
-    dout.release();
     return DGN_OK;
 }
 

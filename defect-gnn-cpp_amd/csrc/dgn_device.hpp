@@ -16,9 +16,15 @@ struct StructMeta {
     double L[9];     // lattice rows a, b, c (row-major)
     double R[9];     // inverse lattice; column k = reciprocal vector of fractional axis k
     double h[3];     // rc * |column k of R|: |frac_k| bound of any vector shorter than rc
+    double H[3];     // h + 1e-9: the conservative fractional half-widths every search uses
     int64_t first;   // first atom (global index)
     int32_t natoms;  // atoms in the structure
     int32_t nref;    // reference image range: ceil(rc / min row norm) + 1 (neighbor_list.cpp:68-72)
+    int32_t one;     // every H_k < 0.5: at most one periodic image of an atom per axis can reach rc
+    int32_t cells;   // a cell list was built (natoms > kStage and one)
+    int32_t nc[3];   // cells per fractional axis (cell list), each cell at least H_k wide
+    int32_t diag;    // lattice rows are axis-aligned (a = (a0,0,0), b = (0,b1,0), c = (0,0,c2))
+    double band;     // |d2_approx - d2| bound of the fixed-point nearest-image distance (x64 margin)
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
@@ -67,6 +73,105 @@ __device__ __forceinline__ T wave_inclusive_sum(T v) {
 }
 
 __device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// One-wave LDS hand-off: a wave's LDS instructions execute in order, so lane-to-lane exchange
+// through LDS only needs the compiler not to move memory operations across this point.
+__device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+__device__ __forceinline__ int tri_c2(int x) { return x * (x - 1) / 2; }
+
+// ---- local distance matrix on the matrix cores (ripser_wrapper.cpp:60-70 + 17-24) ----
+// The K = 3 Gram product as three rank-1 v_mfma_f64_16x16x4_f64 per 16 x 16 tile (operand k'
+// nonzero only for k' == k, so each product is exactly round(x_ik * x_jk)), summed (p0 + p1) + p2
+// on the VALU, then sqrt(max(0, (sq_i + sq_j) - 2 dot)) -> f32: bit-identical to the reference's
+// Eigen path. Writes the strict lower triangle in the reference's packing (row i, j < i at
+// i(i-1)/2 + j). Narrow form: n <= 64, lane p holds cloud row p in px (lanes >= n: any value);
+// sq = per-wave LDS [64].
+__device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, double* sq, float* __restrict__ L) {
+    typedef double double4_t __attribute__((ext_vector_type(4)));
+    const int lane = lane_id();
+    sq[lane] = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
+    const int T = (n + 15) / 16;
+    const int kk = lane >> 4;
+    double xr[4];  // coordinate kk of cloud row 16 I + (lane & 15)
+#pragma unroll
+    for (int I = 0; I < 4; ++I) {
+        const int ra = 16 * I + (lane & 15);
+        const double v0 = __shfl(px[0], ra, kWave), v1 = __shfl(px[1], ra, kWave), v2 = __shfl(px[2], ra, kWave);
+        xr[I] = (ra < n && kk < 3) ? (kk == 0 ? v0 : (kk == 1 ? v1 : v2)) : 0.0;
+    }
+    wave_lds_sync();
+    for (int I = 0; I < T; ++I) {
+        for (int J = 0; J <= I; ++J) {
+            const double xa = I == 0 ? xr[0] : (I == 1 ? xr[1] : (I == 2 ? xr[2] : xr[3]));
+            const double xb = J == 0 ? xr[0] : (J == 1 ? xr[1] : (J == 2 ? xr[2] : xr[3]));
+            const double4_t z = {0.0, 0.0, 0.0, 0.0};
+            const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 0 ? xa : 0.0, kk == 0 ? xb : 0.0, z, 0, 0, 0);
+            const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 1 ? xa : 0.0, kk == 1 ? xb : 0.0, z, 0, 0, 0);
+            const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 2 ? xa : 0.0, kk == 2 ? xb : 0.0, z, 0, 0, 0);
+            const int col = 16 * J + (lane & 15);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * I + (lane >> 4) + 4 * r;
+                if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
+                    const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
+                    const double d2 = (sq[row] + sq[col]) - 2.0 * dot;
+                    L[tri_c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+}
+
+// Wide form (n > 64): row p comes from point(p, x) (x[0..2] = the row's coordinates, static
+// indices only); sq = LDS [n].
+__device__ __forceinline__ double sel3(int k, double a, double b, double c) { return k == 0 ? a : (k == 1 ? b : c); }
+template <class Point>
+__device__ __forceinline__ void gram_triangle_wide(int n, double* sq, float* __restrict__ L, Point&& point) {
+    typedef double double4_t __attribute__((ext_vector_type(4)));
+    const int lane = lane_id();
+    const int kq = lane >> 4;
+    for (int p = lane; p < n; p += kWave) {
+        double x[3];
+        point(p, x);
+        sq[p] = (x[0] * x[0] + x[1] * x[1]) + x[2] * x[2];
+    }
+    wave_lds_sync();
+    const int T = (n + 15) / 16;
+    for (int I = 0; I < T; ++I) {
+        const int ra = 16 * I + (lane & 15);
+        double xa = 0.0;
+        if (ra < n && kq < 3) {
+            double x[3];
+            point(ra, x);
+            xa = sel3(kq, x[0], x[1], x[2]);
+        }
+        for (int J = 0; J <= I; ++J) {
+            const int cb = 16 * J + (lane & 15);
+            double xb = 0.0;
+            if (cb < n && kq < 3) {
+                double x[3];
+                point(cb, x);
+                xb = sel3(kq, x[0], x[1], x[2]);
+            }
+            const double4_t z = {0.0, 0.0, 0.0, 0.0};
+            const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 0 ? xa : 0.0, kq == 0 ? xb : 0.0, z, 0, 0, 0);
+            const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 1 ? xa : 0.0, kq == 1 ? xb : 0.0, z, 0, 0, 0);
+            const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kq == 2 ? xa : 0.0, kq == 2 ? xb : 0.0, z, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 16 * I + (lane >> 4) + 4 * r;
+                if (row < n && cb < row) {
+                    const double dot = (p0[r] + p1[r]) + p2[r];
+                    const double d2 = (sq[row] + sq[cb]) - 2.0 * dot;
+                    L[tri_c2(row) + cb] = (float)sqrt(fmax(d2, 0.0));
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+}
 
 // ---- DPP wave reductions of doubles: row_ror 1/2/4/8 inside each 16-lane row (VALU latency,
 // no LDS round trips), then the four row results by v_readlane ----

@@ -11,15 +11,25 @@ namespace dgn {
 constexpr int kGraphBlock = 256;          // 4 waves
 constexpr int kQA = 64;                   // query atoms per block (16 per wave, round-robin)
 constexpr int kStage = 512;               // structures up to this size are staged in LDS
-constexpr int kRowsMaxK = 64;             // max_neighbors up to this use the stored-rows path
-constexpr int kRowsCap = 128;             // candidates per atom the count pass can rank
+constexpr int kStreamMaxK = 64;           // max_neighbors up to this: block-streamed RBF emit
+constexpr int kCellMax = 4096;            // cells per structure (cell list, natoms > kStage)
 constexpr int kScanThreads = 1024;
+constexpr int kRing = 128;                // per-wave candidate ring (one-image prefilter)
+constexpr int kMaskWords = kStage / 64;   // hit-mask words per query atom (staged structures)
+
+// graph error bits (Scalars::error_flag), decoded in dgn_api.cpp
+constexpr uint32_t kGErrCap = 1u << 0;       // more candidates than the emit capacity
+constexpr uint32_t kGErrMismatch = 1u << 1;  // emit / Betti search disagrees with the count pass
+constexpr uint32_t kGErrFar = 1u << 2;       // a position more than 500 cells away from the origin
 
 struct GraphLaunch {
     const StructMeta* meta;
-    const int32_t* atom_struct;  // [A] structure of each atom (map_atoms_kernel)
+    const int32_t* atom_struct;  // [A] structure of each atom (prep_structures_kernel)
     const int64_t* atom_offset;
     const double* pos;
+    const int32_t* cell_start;   // cell list: [first_b + b + c], c <= ncells (structures with cells)
+    const double4* cell_pos;     // cell-sorted atoms: x, y, z, packed (j, floor of fractional coords)
+    const uint64_t* mask;        // [A][kMaskWords] exact hits of the count pass (staged one-image), or null
     int64_t num_structures, num_atoms;
     double rc2, eps;
     uint64_t kmax;
@@ -29,26 +39,29 @@ struct RbfSpec {
     int32_t dtype;  // DGN_NONE / DGN_F32 / DGN_F64
     int32_t nbins;
     double dr, inv_sigma2, norm;
+    double c2;      // -0.5 * log2(e) / sigma^2 (f32 path exponent scale)
     float inv_nbins, norm_f;
 };
 
-// also fills atom_struct[A] (structure index of every atom)
-hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset,
-                                  int64_t num_structures, double rc, StructMeta* meta, int32_t* atom_struct);
-// per-atom kept counts; per block: block_sums[b] and block_aux[2b] = max candidates,
-// block_aux[2b+1] = sum over atoms of (candidates + 1)^2
-// rows_d/rows_j (optional, [A][max_neighbors]): the ranked kept rows (stored-rows path)
+// Per structure: geometry + the reference image bound + search strategy (thread per structure),
+// then (block per structure) the atom -> structure map, the far-position check, the cell list of
+// structures above kStage atoms and (optional) the per-atom 1/count(species) Betti weight.
+hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset, const double* pos,
+                                  const int32_t* species, int64_t num_structures, double rc, StructMeta* meta,
+                                  int32_t* atom_struct, int32_t* cell_start, double4* cell_pos, double* weight,
+                                  uint32_t* error_flag);
+// per-atom kept counts min(m, kmax); per block: block_sums[b] and block_aux[3b] = max candidates m,
+// block_aux[3b+1] = sum over atoms of (m + 1)^2, block_aux[3b+2] = largest structure;
+// mask_out (optional) [A][kMaskWords]: exact hits of staged one-image structures
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint64_t* block_aux, uint64_t* rows_d, uint64_t* rows_j);
-// streaming emit from stored rows (requires max candidates <= kRowsCap)
-hipError_t launch_graph_emit_rows(hipStream_t s, const GraphLaunch& g, const int32_t* counts,
-                                  const int64_t* block_offsets, const uint64_t* rows_d, const uint64_t* rows_j,
-                                  int64_t* row_ptr, int32_t* col, double* dist, double* disp, void* rbf,
-                                  const RbfSpec& rs);
+                              uint64_t* block_aux, uint64_t* mask_out);
 hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t* block_aux, int64_t nblocks,
-                             int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq);
-// cap: candidate capacity per query atom (>= max candidates from the count pass)
-hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const int32_t* counts,
+                             int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq,
+                             uint32_t* max_natoms);
+// Fused emit: each block re-runs the search for its atoms, ranks, writes row_ptr / col / dist /
+// disp and the RBF. cap >= max candidates of the count pass (64..512); stage = atoms staged in LDS
+// (max structure size if <= kStage, else 0).
+hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag);
 
@@ -59,13 +72,7 @@ int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
 
 // ---- Betti ----
 struct BettiLaunch {
-    const int64_t* row_ptr;   // CSR from the graph emit (K = unlimited), sorted by distance
-    const double* disp;       // [E][3]
-    const double* pos;        // [A][3]
-    const int32_t* species;   // [A]
-    const int64_t* atom_offset;
-    const int32_t* atom_struct;  // atom -> structure (from the neighbour pass) or null
-    int64_t num_structures, num_atoms;
+    int64_t num_atoms;        // complexes of this launch
     float thr;                // (float) r_cutoff
     double* features;         // [A][35]
     int32_t* counts;          // [A][4] or null
@@ -113,7 +120,7 @@ WideLayout betti_wide_layout(int nmax);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax);  // device-wide resident waves (occupancy API)
 
-// distance pass over complexes [first, first + count) of a BettiLaunch's CSR / cloud input
+// distance pass over complexes [first, first + count) of a BettiLaunch's cloud input
 struct DistLaunch {
     int64_t first, count;
     float* lower;      // [count][tri_stride]
@@ -121,8 +128,18 @@ struct DistLaunch {
     double* weight;    // [count]
 };
 hipError_t launch_betti_dist(hipStream_t s, const BettiLaunch& b, const DistLaunch& d);
+// distance pass with its own neighbour search (graph_kernels.hip): complex c = atom first + c,
+// cloud = centre + every neighbour within rc (betti_features.cpp:67-73, NeighborList(rc, inf));
+// writes the packed f32 lower triangle and npoints; counts = the count pass's per-atom m.
+hipError_t launch_betti_dist_search(hipStream_t s, const GraphLaunch& g, int64_t first, int64_t count,
+                                    int max_points, int64_t tri_stride, const int32_t* counts, float* lower,
+                                    int32_t* npoints, uint32_t* error_flag);
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();
+// fresh per-wave scratch: every min-cofacet byte "no cofacet" (0xFF), never a clearing mark
+hipError_t betti_init_scratch(hipStream_t s, uint8_t* base, int slots);
+// fresh wide scratch layout: empty pivot hash tables, u16 min-cofacet tables "no cofacet"
+hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves);
 int betti_grid_waves(int device);
 // side stream for the overflow tier: forked from the launch stream after the bucket pass, joined
 // after the main launch; it owns `overflow_waves` scratch slots past the main grid's

@@ -1,41 +1,63 @@
 // graph_kernels.hip — periodic fixed-radius neighbour search, CSR compaction and Gaussian-RBF
-// edge features for gfx950.
+// edge features for gfx950, plus the Betti pass's local clouds.
 //
 // Replaces src/graph/neighbor_list.cpp:27-94 (nanoflann KD-tree over a (2n+1)^3 image cloud),
-// src/graph/edge_features.cpp:7-24 and the edge loop of src/graph/crystal_graph.cpp:32-40.
+// src/graph/edge_features.cpp:7-24, the edge loop of src/graph/crystal_graph.cpp:32-40 and the
+// NeighborList(rc, SIZE_MAX) + cloud assembly of src/topology/betti_features.cpp:67-73,107.
 //
-// Design (MI355X-first, see DESIGN.md):
-//   * one wave64 per query atom; lane j owns structure atom j of the current 64-atom tile and
-//     enumerates ONLY the periodic images whose fractional slab can reach rc (<= 27 for cells
-//     wider than rc, vs the reference's fixed 125), clamped to the reference's own image range
-//     so the candidate set is exactly the reference's;
-//   * the membership test reproduces the reference arithmetic bit for bit (offset
-//     ((na*a + nb*b) + nc*c), p = pos + offset, d2 = ((dx^2 + dy^2) + dz^2), strict d2 < rc^2,
-//     self-skip sqrt(d2) < eps) — compiled with -ffp-contract=off;
-//   * hits are compacted with ballot + mbcnt into an LDS candidate list, ranked by
-//     (distance, j, image) with broadcast LDS reads, truncated to max_neighbors, and written
-//     to the CSR slot row_ptr[i] + rank;
-//   * the RBF block of an atom (cnt x n_rbf values) is contiguous in HBM and written by the
-//     whole wave in flat, coalesced order; exp is range-reduced in f64 and finished with
-//     v_exp_f32 for the f32 output (|rel err| < 3e-7), or computed in f64 for the f64 output.
-//   * three launches: count (+ per-block sums), block-sum scan, emit (recomputes its rows and
-//     scans its 16 atoms locally). No spin waits.
+// Design (MI355X-first, see DESIGN.md §3.1):
+//   * prep (one block per structure): geometry, the reference's image bound, the atom ->
+//     structure map, the 1/count(species) Betti weight and, for structures above kStage atoms,
+//     a cell list in fractional space (cells at least H wide, so a query's window spans <= 3 cells
+//     per axis);
+//   * one wave64 per query atom; the candidate (atom, image) set is produced by one of three
+//     searches, all conservative supersets of the reference's hits:
+//       - staged + one image per axis (cells wider than 2 rc): the structure's positions and
+//         fractional coordinates are staged in LDS; lane j tests atom j's unique candidate image
+//         with three fractional compares, survivors are ballot-compacted into a per-wave LDS ring
+//         and exact-tested 64 at a time;
+//       - cell list (structures above kStage atoms): lanes enumerate the <= 27 cells of the
+//         window, a wave prefix sum lays their atoms out, lane t exact-tests candidate t;
+//       - general (cells narrower than 2 rc): every image inside the atom's fractional slab;
+//     the exact test reproduces the reference arithmetic bit for bit (offset ((na*a + nb*b) +
+//     nc*c), p = pos + offset, d2 = ((dx^2 + dy^2) + dz^2), strict d2 < rc^2, self skip
+//     sqrt(d2) < eps), clamped to the reference's +-nref image range; -ffp-contract=off;
+//   * count: hit counts only; emit (fused): re-run the search, compact hits with ballot + mbcnt,
+//     rank by (distance, j, image) — the canonical row order; the reference's nanoflann order
+//     differs only among exact ties — and write the kept rows; the block's RBF region (contiguous
+//     in the CSR) is then written as one flat stream of non-temporal 16-byte stores.
 #include "dgn_internal.hpp"
 
 namespace dgn {
 
+constexpr int kW = kGraphBlock / kWave;  // waves per block
+
+__device__ __forceinline__ int32_t uni_i32(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// fractional coordinates u = p . R (R = inverse lattice), one fixed operation order everywhere
+__device__ __forceinline__ double frac_k(const double* R, int k, double x, double y, double z) {
+    return (x * R[k] + y * R[3 + k]) + z * R[6 + k];
+}
+
 // ------------------------------------------------------------------------------------------
-// Structure metadata + atom -> structure map
+// Structure prep: one block per structure
 // ------------------------------------------------------------------------------------------
-__global__ void prep_structures_kernel(const double* __restrict__ lattice, const int64_t* __restrict__ atom_offset,
-                                       int64_t B, double rc, StructMeta* __restrict__ meta) {
+__device__ __forceinline__ uint64_t pack_cell_atom(int j, int s0, int s1, int s2) {
+    return (uint64_t)(uint32_t)j | ((uint64_t)(s0 + 512) << 32) | ((uint64_t)(s1 + 512) << 42) |
+           ((uint64_t)(s2 + 512) << 52);
+}
+
+// thread per structure: geometry + the reference image bound + search strategy
+__global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict__ lattice,
+                                                        const int64_t* __restrict__ atom_offset, int64_t B, double rc,
+                                                        StructMeta* __restrict__ meta) {
     const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     StructMeta m;
     const double* L = lattice + 9 * b;
     for (int k = 0; k < 9; ++k) m.L[k] = L[k];
-    const double a00 = L[0], a01 = L[1], a02 = L[2], a10 = L[3], a11 = L[4], a12 = L[5], a20 = L[6],
-                 a21 = L[7], a22 = L[8];
+    const double a00 = L[0], a01 = L[1], a02 = L[2], a10 = L[3], a11 = L[4], a12 = L[5], a20 = L[6], a21 = L[7],
+                 a22 = L[8];
     const double c00 = a11 * a22 - a12 * a21, c01 = a02 * a21 - a01 * a22, c02 = a01 * a12 - a02 * a11;
     const double c10 = a12 * a20 - a10 * a22, c11 = a00 * a22 - a02 * a20, c12 = a02 * a10 - a00 * a12;
     const double c20 = a10 * a21 - a11 * a20, c21 = a01 * a20 - a00 * a21, c22 = a00 * a11 - a01 * a10;
@@ -44,8 +66,12 @@ __global__ void prep_structures_kernel(const double* __restrict__ lattice, const
     m.R[0] = c00 * id; m.R[1] = c01 * id; m.R[2] = c02 * id;
     m.R[3] = c10 * id; m.R[4] = c11 * id; m.R[5] = c12 * id;
     m.R[6] = c20 * id; m.R[7] = c21 * id; m.R[8] = c22 * id;
-    for (int k = 0; k < 3; ++k)
+    bool one = true;
+    for (int k = 0; k < 3; ++k) {
         m.h[k] = rc * sqrt(m.R[k] * m.R[k] + m.R[3 + k] * m.R[3 + k] + m.R[6 + k] * m.R[6 + k]);
+        m.H[k] = m.h[k] + 1e-9;
+        one = one && m.H[k] < 0.5;
+    }
     // Eigen Matrix3d row norm: x0 + (x1 + x2) (fixed-size unrolled redux), neighbor_list.cpp:69
     double lmin = 1e300;
     for (int r = 0; r < 3; ++r) {
@@ -55,35 +81,193 @@ __global__ void prep_structures_kernel(const double* __restrict__ lattice, const
     m.nref = (int32_t)ceil(rc / lmin) + 1;
     m.first = atom_offset[b];
     m.natoms = (int32_t)(atom_offset[b + 1] - atom_offset[b]);
+    // one image per axis => nref == 2 (rc < half of every perpendicular width < half of every row
+    // norm); the 5^3 image-offset table of the staged search relies on it
+    m.one = (one && m.nref == 2) ? 1 : 0;
+    m.cells = (m.one && m.natoms > kStage) ? 1 : 0;
+    m.diag = (L[1] == 0.0 && L[2] == 0.0 && L[3] == 0.0 && L[5] == 0.0 && L[6] == 0.0 && L[7] == 0.0) ? 1 : 0;
+    // the fixed-point coordinates truncate at 2^-32: the nearest-image displacement is off by at
+    // most 2^-31 (|a| + |b| + |c|) per component, d2 by 2 rc times that (for d <= rc); 64x margin
+    {
+        double lsum = 0.0;
+        for (int r = 0; r < 3; ++r) lsum += fabs(L[3 * r]) + fabs(L[3 * r + 1]) + fabs(L[3 * r + 2]);
+        m.band = 64.0 * 2.0 * rc * lsum * 0x1p-31 + 1e-12 * rc * rc;
+    }
+    for (int k = 0; k < 3; ++k) m.nc[k] = 1;
+    if (m.cells) {
+        // cells at least H wide: a query window (width 2H) spans <= 3 cells per axis
+        int nc[3];
+        for (int k = 0; k < 3; ++k) nc[k] = (int)fmin(floor(1.0 / m.H[k]), 64.0);
+        const int cap = m.natoms < kCellMax ? m.natoms : kCellMax;
+        while ((int64_t)nc[0] * nc[1] * nc[2] > cap) {
+            const int k = nc[0] >= nc[1] && nc[0] >= nc[2] ? 0 : (nc[1] >= nc[2] ? 1 : 2);
+            nc[k] -= 1;
+        }
+        for (int k = 0; k < 3; ++k) m.nc[k] = nc[k];
+    }
     meta[b] = m;
 }
 
-// one block per structure: atom_struct[first .. first + natoms) = b
-__global__ __launch_bounds__(256) void map_atoms_kernel(const int64_t* __restrict__ atom_offset,
-                                                        int32_t* __restrict__ atom_struct) {
+// fractional cell coordinate of atom position p: floor s (the periodic shift of the wrapped
+// coordinate) and the wrapped fraction w in [0, 1) as 32-bit fixed point W (w * 2^32)
+__device__ __forceinline__ void frac_fixed(const double* R, int k, const double p[3], int& s, uint32_t& W) {
+    const double u = frac_k(R, k, p[0], p[1], p[2]);
+    double f = floor(u);
+    uint64_t w = (uint64_t)((u - f) * 4294967296.0);
+    if (w >= 4294967296ull) {  // u - f rounded to 1.0
+        w -= 4294967296ull;
+        f += 1.0;
+    }
+    s = (int)f;
+    W = (uint32_t)w;
+}
+
+// block per structure: atom -> structure map, the far-position check, the per-atom
+// 1/count(species) Betti weight and, for structures above kStage atoms, the cell list
+__global__ __launch_bounds__(256) void prep_atoms_kernel(const StructMeta* __restrict__ meta,
+                                                         const double* __restrict__ pos,
+                                                         const int32_t* __restrict__ species,
+                                                         int32_t* __restrict__ atom_struct,
+                                                         int32_t* __restrict__ cell_start,
+                                                         double4* __restrict__ cell_pos, double* __restrict__ weight,
+                                                         uint32_t* __restrict__ error_flag) {
+    __shared__ int32_t hist[kCellMax + 1];
+    __shared__ int32_t shist[256];
+    __shared__ int32_t part[256 / kWave];
     const int64_t b = blockIdx.x;
-    const int64_t a0 = atom_offset[b], a1 = atom_offset[b + 1];
-    for (int64_t a = a0 + threadIdx.x; a < a1; a += blockDim.x) atom_struct[a] = (int32_t)b;
+    const int tid = threadIdx.x;
+    const StructMeta& sm = meta[b];
+    const int64_t first = sm.first;
+    const int natoms = sm.natoms;
+    const bool one = sm.one != 0;
+    for (int t = tid; t < natoms; t += blockDim.x) {
+        atom_struct[first + t] = (int32_t)b;
+        if (one) {
+            const double* p = pos + 3 * (first + t);
+            bool far = false;
+            for (int k = 0; k < 3; ++k) {
+                const double u = frac_k(sm.R, k, p[0], p[1], p[2]);
+                far = far || !(fabs(u) < 500.0);
+            }
+            if (far) atomicOr(error_flag, kGErrFar);
+        }
+    }
+    // 1 / count(species of i) within the structure (betti_features.cpp:62-63, 77)
+    if (weight && species) {
+        for (int t = tid; t < 256; t += blockDim.x) shist[t] = 0;
+        __syncthreads();
+        for (int t = tid; t < natoms; t += blockDim.x) {
+            const int s = species[first + t];
+            if (s >= 0 && s < 256) atomicAdd(&shist[s], 1);
+        }
+        __syncthreads();
+        for (int t = tid; t < natoms; t += blockDim.x) {
+            const int s = species[first + t];
+            int cnt;
+            if (s >= 0 && s < 256) {
+                cnt = shist[s];
+            } else {
+                cnt = 0;
+                for (int u = 0; u < natoms; ++u) cnt += species[first + u] == s;
+            }
+            weight[first + t] = 1.0 / (double)cnt;
+        }
+    }
+    if (!sm.cells) return;
+    // ---- cell list: counting sort of the atoms by fractional cell ----
+    const int nc0 = sm.nc[0], nc1 = sm.nc[1], nc2 = sm.nc[2];
+    const int ncell = nc0 * nc1 * nc2;
+    for (int c = tid; c <= ncell; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    auto cell_of = [&](int t, int s[3]) -> int {
+        const double* p = pos + 3 * (first + t);
+        int c[3];
+        for (int k = 0; k < 3; ++k) {
+            uint32_t W;
+            frac_fixed(sm.R, k, p, s[k], W);
+            const int n = sm.nc[k];
+            int ck = (int)(((uint64_t)W * (uint64_t)n) >> 32);
+            c[k] = ck < n ? ck : n - 1;
+        }
+        return (c[0] * nc1 + c[1]) * nc2 + c[2];
+    };
+    for (int t = tid; t < natoms; t += blockDim.x) {
+        int s[3];
+        atomicAdd(&hist[cell_of(t, s)], 1);
+    }
+    __syncthreads();
+    // exclusive scan of hist[0 .. ncell) in place: per-thread chunks + wave / block scan
+    const int per = (ncell + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int c0 = tid * per, c1 = c0 + per < ncell ? c0 + per : ncell;
+    int local = 0;
+    for (int c = c0; c < c1; ++c) local += hist[c];
+    const int inc = wave_inclusive_sum(local);
+    if (lane_id() == kWave - 1) part[tid / kWave] = inc;
+    __syncthreads();
+    int off = inc - local;
+    for (int w = 0; w < tid / kWave; ++w) off += part[w];
+    __syncthreads();
+    for (int c = c0; c < c1; ++c) {
+        const int v = hist[c];
+        hist[c] = off;
+        off += v;
+    }
+    __syncthreads();
+    int32_t* cs = cell_start + first + b;
+    for (int c = tid; c < ncell; c += blockDim.x) cs[c] = hist[c];
+    if (tid == 0) cs[ncell] = natoms;
+    __syncthreads();
+    for (int t = tid; t < natoms; t += blockDim.x) {
+        int s[3];
+        const int c = cell_of(t, s);
+        const int slot = atomicAdd(&hist[c], 1);
+        const double* p = pos + 3 * (first + t);
+        cell_pos[first + slot] = make_double4(p[0], p[1], p[2],
+                                              __longlong_as_double((long long)pack_cell_atom(t, s[0], s[1], s[2])));
+    }
 }
 
 // ------------------------------------------------------------------------------------------
-// Block traversal shared by count and emit: a block owns query atoms [g0, g0 + kQA); it walks
-// the structures those atoms belong to, stages each structure's positions in LDS (SoA, when it
-// has at most kStage atoms; larger ones are read from global/L2), and hands every query atom
-// to one wave (atoms round-robin over the 4 waves).
+// Block traversal shared by every search kernel: a block owns query atoms [g0, g1) of the
+// range [a_begin, a_end); it walks the structures those atoms belong to, stages each structure's
+// positions and fractional coordinates in LDS (SoA, when it has at most `cap` atoms; larger ones
+// are read from global/L2), and hands every query atom to one wave (round-robin over the 4).
 // ------------------------------------------------------------------------------------------
-struct StagedPos {
-    double x[kStage], y[kStage], z[kStage];
+// LDS-typed pointers (address space 3): loads through them are ds_read, never flat loads (a flat
+// load's wait also waits for every outstanding global store)
+#define DGN_LDS __attribute__((address_space(3)))
+template <class T>
+__device__ __forceinline__ DGN_LDS T* lds(T* p) { return (DGN_LDS T*)p; }
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+struct StageView {
+    DGN_LDS double *x, *y, *z;  // positions
+    DGN_LDS u32x4* fx;          // fixed-point wrapped fractional coordinates W0, W1, W2 + packed floors
+    DGN_LDS f64x4* offt;        // one-image structures: the 5^3 image offsets ((na*a + nb*b) + nc*c), |n| <= 2
+    int cap;
 };
+// stage bytes per atom: 3 doubles + one uint4
+constexpr int kStageBytesPerAtom = 3 * 8 + 16;
+__device__ __forceinline__ StageView make_stage(double* base_, int cap, double4* offt) {
+    DGN_LDS double* base = lds(base_);
+    return {base, base + cap, base + 2 * cap, reinterpret_cast<DGN_LDS u32x4*>(base + 3 * cap),
+            reinterpret_cast<DGN_LDS f64x4*>(lds(offt)), cap};
+}
+__device__ __forceinline__ uint32_t pack_floors(const int s[3]) {
+    return (uint32_t)(s[0] + 512) | ((uint32_t)(s[1] + 512) << 10) | ((uint32_t)(s[2] + 512) << 20);
+}
+__device__ __forceinline__ int floor_of(uint32_t S, int k) { return (int)((S >> (10 * k)) & 1023u) - 512; }
 
 struct PosSrc {
-    const StagedPos* lds;     // null -> global
-    const double* gpos;       // positions of the structure's first atom
+    StageView st;        // the LDS stage (valid if staged)
+    bool staged;         // false -> global
+    const double* gpos;  // positions of the structure's first atom
     __device__ __forceinline__ void get(int j, double p[3]) const {
-        if (lds) {
-            p[0] = lds->x[j];
-            p[1] = lds->y[j];
-            p[2] = lds->z[j];
+        if (staged) {
+            p[0] = st.x[j];
+            p[1] = st.y[j];
+            p[2] = st.z[j];
         } else {
             p[0] = gpos[3 * j];
             p[1] = gpos[3 * j + 1];
@@ -92,47 +276,305 @@ struct PosSrc {
     }
 };
 
-__device__ __forceinline__ int32_t uni_i32(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// One structure's metadata in wave-uniform registers: lane t loads dword t (one coalesced load),
+// v_readlane moves each dword to an SGPR. (Read through a global pointer the compiler must assume
+// the kernel's own stores may alias it and re-loads every field with vector loads + waits.)
+__device__ __forceinline__ StructMeta load_meta_uniform(const StructMeta* p) {
+    constexpr int N = (int)(sizeof(StructMeta) / 4);
+    static_assert(N <= kWave, "StructMeta must fit one wave load");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p);
+    const int lane = lane_id();
+    const uint32_t v = lane < N ? src[lane] : 0u;
+    StructMeta m;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&m);
+#pragma unroll
+    for (int t = 0; t < N; ++t) dst[t] = (uint32_t)__builtin_amdgcn_readlane((int)v, t);
+    return m;
+}
 
 template <class PerAtom>
-__device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, StagedPos& st, PerAtom&& per_atom) {
-    const int w = threadIdx.x / kWave;
-    const int64_t g0 = (int64_t)blockIdx.x * kQA;
-    const int64_t g1 = g0 + kQA < g.num_atoms ? g0 + kQA : g.num_atoms;
+__device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const StageView st, int64_t a_begin,
+                                                int64_t a_end, PerAtom&& per_atom) {
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int64_t g0 = a_begin + (int64_t)blockIdx.x * kQA;
+    const int64_t g1 = g0 + kQA < a_end ? g0 + kQA : a_end;
+    if (g0 >= g1) return;
     const int32_t b_first = uni_i32(g.atom_struct[g0]);
     const int32_t b_last = uni_i32(g.atom_struct[g1 - 1]);
     for (int32_t b = b_first; b <= b_last; ++b) {
-        const StructMeta& M = g.meta[b];
+        const StructMeta M = load_meta_uniform(g.meta + b);
         const int64_t first = M.first;
         const int natoms = M.natoms;
         if (natoms == 0) continue;
-        const bool staged = natoms <= kStage;
+        const bool staged = natoms <= st.cap;
         if (staged) {
             __syncthreads();  // previous segment done with the stage
             const double* src = g.pos + 3 * first;
             for (int t = threadIdx.x; t < natoms; t += kGraphBlock) {
-                st.x[t] = src[3 * t];
-                st.y[t] = src[3 * t + 1];
-                st.z[t] = src[3 * t + 2];
+                const double p[3] = {src[3 * t], src[3 * t + 1], src[3 * t + 2]};
+                st.x[t] = p[0];
+                st.y[t] = p[1];
+                st.z[t] = p[2];
+                if (M.one) {
+                    int sf[3];
+                    uint32_t W[3];
+                    for (int k = 0; k < 3; ++k) frac_fixed(M.R, k, p, sf[k], W[k]);
+                    const u32x4 v = {W[0], W[1], W[2], pack_floors(sf)};
+                    st.fx[t] = v;
+                }
+            }
+            if (M.one && threadIdx.x < 125) {
+                const int t = threadIdx.x;
+                const double na = (double)(t / 25 - 2), nb = (double)((t / 5) % 5 - 2), nc = (double)(t % 5 - 2);
+                double o[3];
+                for (int k = 0; k < 3; ++k) o[k] = (na * M.L[k] + nb * M.L[3 + k]) + nc * M.L[6 + k];
+                const f64x4 v = {o[0], o[1], o[2], 0.0};
+                st.offt[t] = v;
             }
             __syncthreads();
         }
-        const PosSrc P{staged ? &st : nullptr, g.pos + 3 * first};
+        const PosSrc P{st, staged, g.pos + 3 * first};
         const int64_t s0 = g0 > first ? g0 : first;
         const int64_t s1 = g1 < first + natoms ? g1 : first + natoms;
-        for (int64_t gi = s0 + w; gi < s1; gi += kGraphBlock / kWave) per_atom(M, P, gi, (int)(gi - g0));
+        for (int64_t gi = s0 + w; gi < s1; gi += kW) per_atom(M, P, gi, (int)(gi - g0), (int64_t)b);
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Candidate enumeration: all (j, image) with d2 < rc^2 around query atom q (wave-uniform call).
-// Lane j enumerates only the images whose fractional slab can reach rc, clamped to the
-// reference's +-nref range, with nested counters (no integer division).
-// visit(hit, j, na, nb, nc, d) is invoked by every lane once per step (hit false = idle).
+// Exact candidate test (the reference arithmetic) and the searches.
+// visit(hit, j, na, nb, nc, d2) is invoked by every lane once per step (hit false = idle).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double cand_d2(const StructMeta& M, const double pj[3], int na, int nb, int nc,
+                                          const double q[3]) {
+    const double dna = (double)na, dnb = (double)nb, dnc = (double)nc;
+    double d2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        // offset = (na*a + nb*b) + nc*c (neighbor_list.cpp:82-84); p = pos + offset (:87)
+        const double off = (dna * M.L[k] + dnb * M.L[3 + k]) + dnc * M.L[6 + k];
+        const double diff = q[k] - (pj[k] + off);  // L2_Simple_Adaptor: (a - b)^2 accumulated
+        d2 += diff * diff;
+    }
+    return d2;
+}
+
+__device__ __forceinline__ uint64_t pack_jimg(int j, int na, int nb, int nc) {
+    return ((uint64_t)(uint32_t)j << 24) | ((uint64_t)((na + 128) & 255) << 16) |
+           ((uint64_t)((nb + 128) & 255) << 8) | (uint64_t)((nc + 128) & 255);
+}
+__device__ __forceinline__ void unpack_jimg(uint64_t key, int& j, int& na, int& nb, int& nc) {
+    j = (int)(key >> 24);
+    na = (int)((key >> 16) & 255) - 128;
+    nb = (int)((key >> 8) & 255) - 128;
+    nc = (int)(key & 255) - 128;
+}
+
+// (1) staged structure, one image per axis. With W the 32-bit fixed-point wrapped fractional
+// coordinates, D = W_j - W_q (mod 2^32) read as a signed fraction is the displacement to atom j's
+// nearest image — its only candidate image. Its image n = (s_q - s_j) - carry (s = floors, carry =
+// the wrap of W_j - W_q) and the reference arithmetic (offset from the staged 5^3 table, |n| <=
+// nref = 2) give the exact d2.
+__device__ __forceinline__ double exact_one(const StageView& st, const u32x4 fq, const u32x4 fj, int j,
+                                            const double q[3], int n[3], bool& inr) {
+    inr = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t wj = k == 0 ? fj.x : (k == 1 ? fj.y : fj.z);
+        const uint32_t wq = k == 0 ? fq.x : (k == 1 ? fq.y : fq.z);
+        const int dw = (int)(wj - wq);
+        const int carry = (int)(wj >= wq) - (int)(dw >= 0);
+        n[k] = (floor_of(fq.w, k) - floor_of(fj.w, k)) - carry;
+        inr = inr && (uint32_t)(n[k] + 2) <= 4u;  // |n| <= nref = 2
+    }
+    const f64x4 o = st.offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
+    const double p0 = st.x[j] + o.x, p1 = st.y[j] + o.y, p2 = st.z[j] + o.z;  // p = pos + offset
+    const double e0 = q[0] - p0, e1 = q[1] - p1, e2 = q[2] - p2;
+    return ((0.0 + e0 * e0) + e1 * e1) + e2 * e2;  // L2_Simple_Adaptor accumulation
+}
+// |nearest-image displacement|^2 from the fixed-point coordinates (within M.band of the exact d2)
+__device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq, const u32x4 fj) {
+    const double f0 = (double)(int)(fj.x - fq.x) * 0x1p-32, f1 = (double)(int)(fj.y - fq.y) * 0x1p-32,
+                 f2 = (double)(int)(fj.z - fq.z) * 0x1p-32;
+    double dx, dy, dz;
+    if (M.diag) {
+        dx = f0 * M.L[0];
+        dy = f1 * M.L[4];
+        dz = f2 * M.L[8];
+    } else {
+        dx = (f0 * M.L[0] + f1 * M.L[3]) + f2 * M.L[6];
+        dy = (f0 * M.L[1] + f1 * M.L[4]) + f2 * M.L[7];
+        dz = (f0 * M.L[2] + f1 * M.L[5]) + f2 * M.L[8];
+    }
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+// Count pass on a staged one-image structure: lane j decides atom j from the approximate distance;
+// only candidates within the band around rc (a handful per million) take the exact reference
+// test. The self image (j == li, n = 0) is the only image of the query atom within rc. Returns
+// m; mask[t] = the hit ballot of atom tile t (a bit per atom).
+__device__ __forceinline__ int count_staged_one(const StructMeta& M, const StageView st, const double q[3], int li,
+                                                double rc2, DGN_LDS uint64_t* mask_words) {
+    const int lane = lane_id();
+    const int natoms = M.natoms;
+    const u32x4 fq = st.fx[li];
+    const double lo = rc2 - M.band, hi = rc2 + M.band;
+    int m = 0;
+    for (int base = 0, t = 0; base < natoms; base += kWave, ++t) {
+        const int j = base + lane;
+        bool hit = false;
+        if (j < natoms && j != li) {
+            const u32x4 fj = st.fx[j];
+            const double d2a = approx_d2(M, fq, fj);
+            hit = d2a < lo;
+            if (d2a >= lo && d2a <= hi) {  // borderline: the exact reference arithmetic decides
+                int n[3];
+                bool inr;
+                const double d2 = exact_one(st, fq, fj, j, q, n, inr);
+                hit = inr && d2 < rc2;
+            }
+        }
+        const uint64_t bal = ballot(hit);
+        if (mask_words && lane == 0) mask_words[t] = bal;
+        m += __popcll(bal);
+    }
+    return m;
+}
+
+// Hit collection on a staged one-image structure (emit / Betti): `produce(base, lane, fq) -> bool`
+// marks the candidates of atom tile [base, base + 64) — the count pass's exact hit mask, or the
+// approximate test (hit or borderline); they queue in a per-wave LDS ring and are exact-tested 64
+// at a time.
+template <class Produce, class Visit>
+__device__ __forceinline__ void search_staged_one(const StructMeta& M, const StageView st, const double q[3], int li,
+                                                  double rc2, double eps, DGN_LDS uint32_t* ring, Produce&& produce,
+                                                  Visit&& visit) {
+    const int lane = lane_id();
+    const int natoms = M.natoms;
+    const u32x4 fq = st.fx[li];
+    int head = 0, cnt = 0;
+    auto flush = [&](int take) {
+        wave_lds_sync();
+        const bool valid = lane < take;
+        const int j = valid ? (int)ring[(head + lane) & (kRing - 1)] : li;
+        const u32x4 fj = st.fx[j];
+        int n[3];
+        bool inr;
+        const double d2 = exact_one(st, fq, fj, j, q, n, inr);
+        bool hit = valid && inr && d2 < rc2;         // RadiusResultSet: strict
+        if (hit && j == li) hit = !(sqrt(d2) < eps);  // self skip (neighbor_list.cpp:47)
+        visit(hit, j, n[0], n[1], n[2], d2);
+        head = (head + take) & (kRing - 1);
+        cnt -= take;
+        wave_lds_sync();
+    };
+    for (int base = 0; base < natoms; base += kWave) {
+        const int j = base + lane;
+        const bool pass = j < natoms && produce(base, lane, fq);
+        const uint64_t bal = ballot(pass);
+        if (pass) ring[(head + cnt + mask_prefix(bal)) & (kRing - 1)] = (uint32_t)j;
+        cnt += __popcll(bal);
+        if (cnt >= kWave) flush(kWave);
+    }
+    while (cnt > 0) flush(cnt < kWave ? cnt : kWave);
+}
+
+// the approximate test of atom base + lane (hit or borderline; the exact test decides)
+struct ApproxOne {
+    StageView st;
+    StructMeta M;
+    int li;
+    __device__ __forceinline__ bool operator()(int base, int lane, const u32x4 fq) const {
+        const int j = base + lane;
+        return j != li && approx_d2(M, fq, st.fx[j]) <= rc2_ + M.band;
+    }
+    double rc2_;
+};
+// the count pass's exact hits of this query (one bit per atom): lane t holds word t (one
+// coalesced load per query), each tile reads its word with v_readlane
+struct FromMask {
+    uint32_t lo, hi;  // word lane_id() of this atom's mask
+    __device__ __forceinline__ bool operator()(int base, int lane, const u32x4) const {
+        const uint32_t wl = (uint32_t)__builtin_amdgcn_readlane((int)lo, base >> 6);
+        const uint32_t wh = (uint32_t)__builtin_amdgcn_readlane((int)hi, base >> 6);
+        return ((lane < 32 ? wl : wh) >> (lane & 31)) & 1u;
+    }
+};
+__device__ __forceinline__ FromMask load_mask(const DGN_LDS uint64_t* m, int natoms) {
+    const int lane = lane_id();
+    const uint64_t w = lane < (natoms + 63) / 64 ? m[lane] : 0ull;
+    return {(uint32_t)w, (uint32_t)(w >> 32)};
+}
+
+// (2) cell list (structures above kStage atoms, one image per axis)
 template <class Visit>
-__device__ __forceinline__ void for_each_candidate(const StructMeta& M, const PosSrc& P, const double q[3], int li,
-                                                   double rc2, double eps, Visit&& visit) {
+__device__ __forceinline__ void search_cells(const GraphLaunch& g, const StructMeta& M, int64_t b, const double q[3],
+                                             int li, Visit&& visit) {
+    const int lane = lane_id();
+    const int nc0 = M.nc[0], nc1 = M.nc[1], nc2 = M.nc[2];
+    int lo[3], cw[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double u = frac_k(M.R, k, q[0], q[1], q[2]);
+        const double n = (double)M.nc[k];
+        lo[k] = (int)floor((u - M.H[k]) * n);
+        cw[k] = (int)floor((u + M.H[k]) * n) - lo[k] + 1;
+    }
+    const int ncv = cw[0] * cw[1] * cw[2];  // <= 64: each cell is at least H wide
+    const int32_t* cs = g.cell_start + M.first + b;
+    const double4* cp = g.cell_pos + M.first;
+    int start = 0, len = 0, img0 = 0, img1 = 0, img2 = 0;
+    if (lane < ncv) {
+        const int plane = cw[1] * cw[2];
+        const int a = lane / plane, r = lane - a * plane, bb = r / cw[2], c = r - bb * cw[2];
+        const int C0 = lo[0] + a, C1 = lo[1] + bb, C2 = lo[2] + c;
+        const int w0 = ((C0 % nc0) + nc0) % nc0, w1 = ((C1 % nc1) + nc1) % nc1, w2 = ((C2 % nc2) + nc2) % nc2;
+        img0 = (C0 - w0) / nc0;
+        img1 = (C1 - w1) / nc1;
+        img2 = (C2 - w2) / nc2;
+        const int cid = (w0 * nc1 + w1) * nc2 + w2;
+        start = cs[cid];
+        len = cs[cid + 1] - start;
+    }
+    const int incl = wave_inclusive_sum(len);
+    const int total = __shfl(incl, kWave - 1, kWave);
+    const int nref = M.nref;
+    for (int t0 = 0; t0 < total; t0 += kWave) {
+        const int t = t0 + lane;
+        // owning cell: the first lane whose inclusive end exceeds t
+        int L = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int probe = __shfl(incl, L + step - 1, kWave);
+            L += probe <= t ? step : 0;
+        }
+        const int cst = __shfl(start, L, kWave), cin = __shfl(incl, L, kWave), cln = __shfl(len, L, kWave);
+        const int i0 = __shfl(img0, L, kWave), i1 = __shfl(img1, L, kWave), i2 = __shfl(img2, L, kWave);
+        bool hit = false;
+        double d2 = 0.0;
+        int j = 0, na = 0, nb = 0, nc = 0;
+        if (t < total) {
+            const double4 rec = cp[cst + (t - (cin - cln))];
+            const uint64_t pk = (uint64_t)__double_as_longlong(rec.w);
+            j = (int)(uint32_t)pk;
+            na = i0 - ((int)((pk >> 32) & 1023) - 512);
+            nb = i1 - ((int)((pk >> 42) & 1023) - 512);
+            nc = i2 - ((int)((pk >> 52) & 1023) - 512);
+            if (abs(na) <= nref && abs(nb) <= nref && abs(nc) <= nref) {
+                const double pj[3] = {rec.x, rec.y, rec.z};
+                d2 = cand_d2(M, pj, na, nb, nc, q);
+                hit = d2 < g.rc2;
+                if (hit && j == li) hit = !(sqrt(d2) < g.eps);
+            }
+        }
+        visit(hit, j, na, nb, nc, d2);
+    }
+}
+
+// (3) general: lane j enumerates every image whose fractional slab can reach rc, clamped to the
+// reference's +-nref range, with nested counters (no integer division)
+template <class Visit>
+__device__ __forceinline__ void search_general(const StructMeta& M, const PosSrc& P, const double q[3], int li,
+                                               double rc2, double eps, Visit&& visit) {
     const int lane = lane_id();
     const int natoms = M.natoms;
     for (int base = 0; base < natoms; base += kWave) {
@@ -147,8 +589,8 @@ __device__ __forceinline__ void for_each_candidate(const StructMeta& M, const Po
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const double df = r0 * M.R[k] + r1 * M.R[3 + k] + r2 * M.R[6 + k];
-                int l = (int)ceil(-df - M.h[k] - 1e-9);
-                int h = (int)floor(-df + M.h[k] + 1e-9);
+                int l = (int)ceil(-df - M.H[k]);
+                int h = (int)floor(-df + M.H[k]);
                 l = l < -M.nref ? -M.nref : l;
                 h = h > M.nref ? M.nref : h;
                 lo[k] = l;
@@ -159,22 +601,12 @@ __device__ __forceinline__ void for_each_candidate(const StructMeta& M, const Po
         int na = lo[0], nb = lo[1], nc = lo[2];
         for (int t = 0; ballot(t < ni); ++t) {
             bool hit = false;
-            double d = 0.0;
+            double d2 = 0.0;
             const int ca = na, cb = nb, cc = nc;
             if (t < ni) {
-                const double dna = (double)ca, dnb = (double)cb, dnc = (double)cc;
-                double d2 = 0.0;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    // offset = (na*a + nb*b) + nc*c (neighbor_list.cpp:82-84); p = pos + offset (:87)
-                    const double off = (dna * M.L[k] + dnb * M.L[3 + k]) + dnc * M.L[6 + k];
-                    const double diff = q[k] - (p[k] + off);  // L2_Simple_Adaptor: (a - b)^2 accumulated
-                    d2 += diff * diff;
-                }
-                if (d2 < rc2) {  // RadiusResultSet: strict
-                    d = sqrt(d2);
-                    hit = !(j == li && d < eps);  // self skip (neighbor_list.cpp:47)
-                }
+                d2 = cand_d2(M, p, ca, cb, cc, q);
+                hit = d2 < rc2;
+                if (hit && j == li) hit = !(sqrt(d2) < eps);
                 if (++nc > hi[2]) {
                     nc = lo[2];
                     if (++nb > hi[1]) {
@@ -183,115 +615,103 @@ __device__ __forceinline__ void for_each_candidate(const StructMeta& M, const Po
                     }
                 }
             }
-            visit(hit, j, ca, cb, cc, d);
+            visit(hit, j, ca, cb, cc, d2);
         }
     }
 }
 
-__device__ __forceinline__ uint64_t pack_jimg(int j, int na, int nb, int nc) {
-    return ((uint64_t)(uint32_t)j << 24) | ((uint64_t)((na + 128) & 255) << 16) |
-           ((uint64_t)((nb + 128) & 255) << 8) | (uint64_t)((nc + 128) & 255);
-}
-
-// ------------------------------------------------------------------------------------------
-// Ranking of one atom's compacted candidates by (distance, j, image) — the canonical row order
-// (the reference's nanoflann order differs only among exact ties). Lane s ranks entry s by
-// counting smaller keys (broadcast LDS reads); visit(rank, kd, kj) for every entry.
-// ------------------------------------------------------------------------------------------
+// mask: the count pass's exact hits of this query (staged one-image structures), or null = search
 template <class Visit>
-__device__ __forceinline__ void rank_candidates(const uint64_t* kd_, const uint64_t* kj_, int m, Visit&& visit) {
-    for (int s = lane_id(); s < m; s += kWave) {
-        const uint64_t kd = kd_[s], kj = kj_[s];
-        int rank = 0;
-        for (int u = 0; u < m; ++u) {
-            const uint64_t ud = kd_[u], uj = kj_[u];
-            rank += (ud < kd) | ((ud == kd) & (uj < kj));
-        }
-        visit(rank, kd, kj);
+__device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M, int64_t b, const PosSrc& P,
+                                       const double q[3], int li, DGN_LDS uint32_t* ring,
+                                       const DGN_LDS uint64_t* mask, Visit&& visit) {
+    if (M.one && P.staged) {
+        if (mask) search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, load_mask(mask, M.natoms), visit);
+        else search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, ApproxOne{P.st, M, li, g.rc2}, visit);
+    } else if (M.one && M.cells) {
+        search_cells(g, M, b, q, li, visit);
+    } else {
+        search_general(M, P, q, li, g.rc2, g.eps, visit);
     }
 }
 
+// shared memory of every staged search kernel: the stage (dynamic or static), the image-offset
+// table and the per-wave candidate rings
+#define DGN_SEARCH_SMEM                        \
+    __shared__ double4 offt_s[125];            \
+    __shared__ uint32_t ring[kW][kRing];
+
 // ------------------------------------------------------------------------------------------
-// Kernel 1: per-atom kept counts + per-block (sum, max candidates, sum (m+1)^2). No atomics.
-// ROWS: also rank each atom's candidates and store its kept rows (distance bits, packed
-// j/image) at rows[gi * K + rank], K = max_neighbors <= kRowsMaxK, so the emit pass only
-// streams; atoms with more than kRowsCap candidates set the block's overflow bit instead.
+// Kernel 1: per-atom kept counts + per-block (sum, max candidates, sum (m+1)^2, max structure
+// size). No atomics. For staged one-image structures it also records each query's exact hits as
+// a bit per atom (mask[gi][kMaskWords]) so the emit and Betti passes skip the search.
 // ------------------------------------------------------------------------------------------
-template <bool ROWS>
 __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
                                                                    int64_t* __restrict__ block_sums,
                                                                    uint64_t* __restrict__ block_aux,
-                                                                   uint64_t* __restrict__ rows_d,
-                                                                   uint64_t* __restrict__ rows_j) {
-    constexpr int W = kGraphBlock / kWave;
-    constexpr int CAP = ROWS ? kRowsCap : 1;
-    __shared__ StagedPos st;
-    __shared__ int64_t wsum[W];
-    __shared__ uint64_t wmax[W], wsq[W];
-    __shared__ uint64_t key_d[W][CAP];
-    __shared__ uint64_t key_j[W][CAP];
+                                                                   uint64_t* __restrict__ mask_out) {
+    __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
+    DGN_SEARCH_SMEM
+    __shared__ int32_t cnt_s[kQA], nw_s[kQA];        // block outputs, written at the end (no global
+    __shared__ uint64_t mask_s[kQA][kMaskWords];     // memory inside the per-query loop)
+    __shared__ int64_t wsum[kW];
+    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW];
+    const StageView st = make_stage(stage_mem, kStage, offt_s);
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
+    const int64_t g0 = (int64_t)blockIdx.x * kQA;
     int64_t my_sum = 0;
-    uint32_t my_max = 0;
+    uint32_t my_max = 0, my_nat = 0;
     uint64_t my_sq = 0;
-    for_block_atoms(g, st, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int) {
+    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
-        int m = 0;
-        if constexpr (ROWS) {
-            for_each_candidate(M, P, q, li, g.rc2, g.eps, [&](bool hit, int j, int na, int nb, int nc, double d) {
-                const uint64_t bal = ballot(hit);
-                if (hit) {
-                    const int slot = m + mask_prefix(bal);
-                    if (slot < CAP) {
-                        key_d[w][slot] = f64_bits(d);
-                        key_j[w][slot] = pack_jimg(j, na, nb, nc);
-                    }
-                }
-                m += __popcll(bal);
-            });
+        int m = 0, nw = 0;
+        if (M.one && P.staged) {
+            m = count_staged_one(M, P.st, q, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr);
+            nw = mask_out ? (M.natoms + 63) / 64 : 0;
         } else {
-            for_each_candidate(M, P, q, li, g.rc2, g.eps,
-                               [&](bool hit, int, int, int, int, double) { m += __popcll(ballot(hit)); });
+            search(g, M, b, P, q, li, lds(ring[w]), nullptr,
+                   [&](bool hit, int, int, int, int, double) { m += __popcll(ballot(hit)); });
         }
         const int64_t c = (uint64_t)m < g.kmax ? (int64_t)m : (int64_t)g.kmax;
-        if (lane == 0) counts[gi] = (int32_t)c;
-        if constexpr (ROWS) {
-            if (m <= CAP) {
-                __builtin_amdgcn_wave_barrier();
-                const int64_t base = gi * (int64_t)g.kmax;
-                rank_candidates(key_d[w], key_j[w], m, [&](int rank, uint64_t kd, uint64_t kj) {
-                    if (rank < c) {
-                        rows_d[base + rank] = kd;
-                        rows_j[base + rank] = kj;
-                    }
-                });
-                __builtin_amdgcn_wave_barrier();
-            }
+        if (lane == 0) {
+            cnt_s[t] = (int32_t)c;
+            nw_s[t] = nw;
         }
         my_sum += c;
         my_max = (uint32_t)m > my_max ? (uint32_t)m : my_max;
+        my_nat = (uint32_t)M.natoms > my_nat ? (uint32_t)M.natoms : my_nat;
         my_sq += (uint64_t)(m + 1) * (uint64_t)(m + 1);  // local-complex n^2
     });
     if (lane == 0) {
         wsum[w] = my_sum;
         wmax[w] = my_max;
         wsq[w] = my_sq;
+        wnat[w] = my_nat;
     }
     __syncthreads();
+    const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
+    for (int i = threadIdx.x; i < nq; i += kGraphBlock) counts[g0 + i] = cnt_s[i];
+    if (mask_out)
+        for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock) {
+            const int a_ = x / kMaskWords, wd = x % kMaskWords;
+            if (wd < nw_s[a_]) mask_out[(g0 + a_) * kMaskWords + wd] = mask_s[a_][wd];
+        }
     if (threadIdx.x == 0) {
         int64_t s = 0;
-        uint64_t mx = 0, sq = 0;
-        for (int k = 0; k < W; ++k) {
+        uint64_t mx = 0, sq = 0, nat = 0;
+        for (int k = 0; k < kW; ++k) {
             s += wsum[k];
             mx = wmax[k] > mx ? wmax[k] : mx;
+            nat = wnat[k] > nat ? wnat[k] : nat;
             sq += wsq[k];
         }
         block_sums[blockIdx.x] = s;
-        block_aux[2 * blockIdx.x] = mx;
-        block_aux[2 * blockIdx.x + 1] = sq;
+        block_aux[3 * blockIdx.x] = mx;
+        block_aux[3 * blockIdx.x + 1] = sq;
+        block_aux[3 * blockIdx.x + 2] = nat;
     }
 }
 
@@ -303,20 +723,22 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
                                                                   const uint64_t* __restrict__ aux, int64_t n,
                                                                   int64_t* __restrict__ total,
                                                                   uint32_t* __restrict__ max_candidates,
-                                                                  unsigned long long* __restrict__ sum_sq) {
+                                                                  unsigned long long* __restrict__ sum_sq,
+                                                                  uint32_t* __restrict__ max_natoms) {
     __shared__ int64_t wtot[kScanThreads / kWave];
-    __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave];
+    __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave], wna[kScanThreads / kWave];
     __shared__ int64_t carry_s;
     const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
     if (tid == 0) carry_s = 0;
-    uint64_t mx = 0, sq = 0;
+    uint64_t mx = 0, sq = 0, na = 0;
     __syncthreads();
     for (int64_t base = 0; base < n; base += kScanThreads) {
         const int64_t i = base + tid;
         const int64_t x = i < n ? v[i] : 0;
         if (i < n) {
-            mx = aux[2 * i] > mx ? aux[2 * i] : mx;
-            sq += aux[2 * i + 1];
+            mx = aux[3 * i] > mx ? aux[3 * i] : mx;
+            sq += aux[3 * i + 1];
+            na = aux[3 * i + 2] > na ? aux[3 * i + 2] : na;
         }
         const int64_t inc = wave_inclusive_sum(x);
         if (lane == kWave - 1) wtot[w] = inc;
@@ -331,42 +753,88 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
     }
     mx = wave_max(mx);
     sq = wave_sum(sq);
+    na = wave_max(na);
     if (lane == 0) {
         wmx[w] = mx;
         wsq[w] = sq;
+        wna[w] = na;
     }
     __syncthreads();
     if (tid == 0) {
         *total = carry_s;
-        uint64_t m = 0, s = 0;
+        uint64_t m = 0, s = 0, a = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) {
             m = wmx[k] > m ? wmx[k] : m;
             s += wsq[k];
+            a = wna[k] > a ? wna[k] : a;
         }
         *max_candidates = (uint32_t)m;
         *sum_sq = s;
+        *max_natoms = (uint32_t)a;
     }
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 3: emit CSR rows + edge features.
+// Ranking of one atom's compacted hits by (distance, j, image), the canonical row order.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float rbf_value_f32(double d, int k, const RbfSpec& r) {
-    const double center = k * r.dr;  // edge_features.cpp:20
-    const double t = center - d;
-    const double arg = -0.5 * (t * t) * r.inv_sigma2;  // -0.5 * pow(c - d, 2) * inv_sigma_squared
-    const double x = arg * 1.4426950408889634074;      // log2(e)
-    const double n = rint(x);
-    const float e = __builtin_amdgcn_exp2f((float)(x - n));  // |x - n| <= 0.5
-    return (float)(r.norm * ldexp((double)e, (int)n));
+// m <= 64: lane s ranks entry s by counting strictly smaller distances (broadcast LDS reads, one
+// f64 compare each); exact distance ties collide on a rank, which a claim byte detects, and only
+// then is the (j, image) tie-break counted.
+__device__ __forceinline__ int rank_small(const DGN_LDS double* kd, const DGN_LDS uint64_t* kj, int m,
+                                          DGN_LDS uint8_t* claim) {
+    const int lane = lane_id();
+    const bool act = lane < m;
+    const double me = act ? kd[lane] : 0.0;
+    int r = 0, u = 0;
+    for (; u + 4 <= m; u += 4) {
+        const double a = kd[u], b = kd[u + 1], c = kd[u + 2], e = kd[u + 3];
+        r += (int)(a < me) + (int)(b < me) + (int)(c < me) + (int)(e < me);
+    }
+    for (; u < m; ++u) r += (int)(kd[u] < me);
+    if (act) claim[r] = (uint8_t)lane;
+    wave_lds_sync();
+    const bool lost = act && claim[r] != (uint8_t)lane;
+    if (ballot(lost)) {
+        const uint64_t mj = act ? kj[lane] : 0ull;
+        int extra = 0;
+        for (u = 0; u < m; ++u) extra += (int)((kd[u] == me) & (kj[u] < mj));
+        r += extra;
+    }
+    return r;
+}
+// m > 64: lane s ranks entries s, s + 64, ... with the full key (broadcast LDS reads)
+template <class Visit>
+__device__ __forceinline__ void rank_large(const DGN_LDS double* kd, const DGN_LDS uint64_t* kj, int m, Visit&& visit) {
+    for (int s = lane_id(); s < m; s += kWave) {
+        const double d = kd[s];
+        const uint64_t j = kj[s];
+        int rank = 0;
+        for (int u = 0; u < m; ++u) {
+            const double ud = kd[u];
+            const uint64_t uj = kj[u];
+            rank += (int)((ud < d) | ((ud == d) & (uj < j)));
+        }
+        visit(rank, d, j);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// RBF values (edge_features.cpp:7-24): g_k(d) = norm * exp(-0.5 (k dr - d)^2 / sigma^2)
+// ------------------------------------------------------------------------------------------
+// f32 output: t = k dr - d in f64; the exponent x = t^2 * c2 (c2 = -0.5 log2(e) / sigma^2, |x| <=
+// 6.5 because |t| <= rc = 3 sigma) in f64, rounded to f32 once (abs error <= 2.4e-7), v_exp_f32
+// (1 ulp), times the f32 normaliser: |rel err| < 4.1e-7 against the f64 value.
+__device__ __forceinline__ float rbf_f32(double t, const RbfSpec& r) {
+    const float x = (float)((t * t) * r.c2);
+    return __builtin_amdgcn_exp2f(x) * r.norm_f;
 }
 __device__ __forceinline__ double rbf_value_f64(double d, int k, const RbfSpec& r) {
-    const double center = k * r.dr;
+    const double center = k * r.dr;  // edge_features.cpp:20
     const double t = center - d;
     return r.norm * exp(-0.5 * (t * t) * r.inv_sigma2);
 }
 
-// flat element f of an atom's RBF block -> (edge, bin); exact for f < 2^24
+// flat element f of an edge block -> (edge, bin); exact for f < 2^24
 __device__ __forceinline__ void rbf_split(int f, const RbfSpec& r, int& e, int& k) {
     e = (int)((float)f * r.inv_nbins);
     if (e * r.nbins > f) --e;
@@ -374,59 +842,99 @@ __device__ __forceinline__ void rbf_split(int f, const RbfSpec& r, int& e, int& 
     k = f - e * r.nbins;
 }
 
-// write the kept x nbins RBF block of one atom: scalar head to a 16-byte boundary, 16-byte
-// vector body, scalar tail (all lanes of the wave, coalesced)
+// Write the RBF of `total` = edges x nbins flat values starting at `out` from the edge distances
+// sd[] with `threads` cooperating threads (thread index tix): scalar head to a 16-byte boundary,
+// non-temporal 16-byte body (written once, never re-read here), scalar tail.
 template <typename T>
-__device__ __forceinline__ void write_rbf_block(T* __restrict__ out, int total, const double* sd, const RbfSpec& rs) {
+__device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, const DGN_LDS double* sd, const RbfSpec& rs,
+                                               int tix, int threads) {
     constexpr int V = 16 / sizeof(T);
-    const int lane = lane_id();
+    const int nb = rs.nbins;
     const int mis = (int)(((uintptr_t)out / sizeof(T)) & (V - 1));
     int head = mis ? V - mis : 0;
     head = head < total ? head : total;
-    auto val = [&](int f) -> T {
+    auto one = [&](int f) -> T {
         int e, k;
         rbf_split(f, rs, e, k);
-        if constexpr (sizeof(T) == 4) return rbf_value_f32(sd[e], k, rs);
+        if constexpr (sizeof(T) == 4) return rbf_f32((double)k * rs.dr - sd[e], rs);
         else return rbf_value_f64(sd[e], k, rs);
     };
-    if (lane < head) out[lane] = val(lane);
+    if (tix < head) out[tix] = one(tix);
     const int nvec = (total - head) / V;
-    for (int v = lane; v < nvec; v += kWave) {
+    for (int v = tix; v < nvec; v += threads) {
         const int f = head + V * v;
+        int e, k;
+        rbf_split(f, rs, e, k);
         if constexpr (sizeof(T) == 4) {
-            float4 o;
-            o.x = val(f);
-            o.y = val(f + 1);
-            o.z = val(f + 2);
-            o.w = val(f + 3);
-            *reinterpret_cast<float4*>(out + f) = o;
+            double d = sd[e];
+            double t = (double)k * rs.dr - d;
+            float o[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                o[u] = rbf_f32(t, rs);
+                if (++k == nb) {
+                    k = 0;
+                    d = sd[++e];  // sd has one slack entry past the last edge
+                    t = -d;
+                } else {
+                    t += rs.dr;
+                }
+            }
+            typedef float float4_t __attribute__((ext_vector_type(4)));
+            const float4_t ov = {o[0], o[1], o[2], o[3]};
+            __builtin_nontemporal_store(ov, reinterpret_cast<float4_t*>(out + f));
         } else {
-            double2 o;
-            o.x = val(f);
-            o.y = val(f + 1);
-            *reinterpret_cast<double2*>(out + f) = o;
+            double o[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                o[u] = rbf_value_f64(sd[e], k, rs);
+                if (++k == nb) {
+                    k = 0;
+                    ++e;
+                }
+            }
+            typedef double double2_t __attribute__((ext_vector_type(2)));
+            const double2_t ov = {o[0], o[1]};
+            __builtin_nontemporal_store(ov, reinterpret_cast<double2_t*>(out + f));
         }
     }
-    const int tail0 = head + V * nvec;
-    if (tail0 + lane < total) out[tail0 + lane] = val(tail0 + lane);
+    const int t0 = head + V * nvec;
+    if (t0 + tix < total) out[t0 + tix] = one(t0 + tix);
 }
 
-template <int CAP>
-__global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, const int32_t* __restrict__ counts,
+// ------------------------------------------------------------------------------------------
+// Kernel 3: fused emit. Per atom (one wave): search, compact the hits into LDS, rank, write the
+// kept rows (col, distance, displacement). STREAM (max_neighbors <= kStreamMaxK): the kept
+// distances of the block's edges are kept in LDS and, after the block's atoms are done, its whole
+// RBF region (contiguous in the CSR) is written as one flat stream by all 256 threads; otherwise
+// each wave writes its atom's RBF block.
+// ------------------------------------------------------------------------------------------
+template <int CAP, bool STREAM>
+__global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, int stage_cap,
+                                                                  const int32_t* __restrict__ counts,
                                                                   const int64_t* __restrict__ block_offsets,
                                                                   int64_t* __restrict__ row_ptr,
                                                                   int32_t* __restrict__ col, double* __restrict__ dist,
                                                                   double* __restrict__ disp, void* __restrict__ rbf,
                                                                   RbfSpec rs, uint32_t* __restrict__ error_flag) {
-    constexpr int W = kGraphBlock / kWave;
-    __shared__ StagedPos st;
-    __shared__ uint64_t key_d[W][CAP];
-    __shared__ uint64_t key_j[W][CAP];
-    __shared__ double sorted_d[W][CAP];
-    __shared__ int64_t row_start[kQA];
+    // dynamic: the stage [stage_cap atoms]; STREAM: the block's edge distances [kQA * K + 1] and
+    // columns [kQA * K] (written to HBM once the block's atoms are done, coalesced)
+    extern __shared__ double dyn[];
+    DGN_SEARCH_SMEM
+    __shared__ double key_d[kW][CAP];
+    __shared__ uint64_t key_j[kW][CAP];
+    __shared__ double sorted_d[kW][STREAM ? 1 : CAP + 1];
+    __shared__ uint8_t claim[kW][kWave];
+    __shared__ int64_t row_start[kQA + 1];
+    __shared__ uint64_t mask_s[kQA][kMaskWords];
+    const StageView st = make_stage(dyn, stage_cap, offt_s);
+    const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
+    DGN_LDS double* dl = lds(dyn) + stage_cap * kStageBytesPerAtom / 8;
+    DGN_LDS int32_t* colb = reinterpret_cast<DGN_LDS int32_t*>(dl + (STREAM ? kQA * K + 1 : 0));
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
     const int64_t g0 = (int64_t)blockIdx.x * kQA;
+    const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
 
     // local scan of this block's counts -> row starts (and row_ptr); kQA == one wave
     if (w == 0) {
@@ -435,211 +943,209 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         const int64_t inc = wave_inclusive_sum(c);
         const int64_t start = block_offsets[blockIdx.x] + inc - c;
         row_start[lane] = start;
-        if (gi < g.num_atoms) {
-            row_ptr[gi] = start;
-            if (gi == g.num_atoms - 1) row_ptr[g.num_atoms] = start + c;
-        }
-    }
-    __syncthreads();
-    for_block_atoms(g, st, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t) {
-        const int li = (int)(gi - M.first);
-        double q[3];
-        P.get(li, q);
-        // 1. compact hits into the wave's LDS candidate list
-        int m = 0;
-        for_each_candidate(M, P, q, li, g.rc2, g.eps, [&](bool hit, int j, int na, int nb, int nc, double d) {
-            const uint64_t bal = ballot(hit);
-            if (hit) {
-                const int slot = m + mask_prefix(bal);
-                if (slot < CAP) {
-                    key_d[w][slot] = f64_bits(d);
-                    key_j[w][slot] = pack_jimg(j, na, nb, nc);
-                }
-            }
-            m += __popcll(bal);
-        });
-        const int cnt = counts[gi];
-        const int64_t rs0 = row_start[t];
-        const int kept = (uint64_t)m < g.kmax ? m : (int)g.kmax;
-        if (m > CAP || kept != cnt) {
-            if (lane == 0) atomicOr(error_flag, m > CAP ? 1u : 2u);
-            return;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // 2. rank by (distance, j, image) and write the kept rows
-        rank_candidates(key_d[w], key_j[w], m, [&](int rank, uint64_t kd, uint64_t kj) {
-            if (rank < kept) {
-                const int64_t e = rs0 + rank;
-                const int j = (int)(kj >> 24);
-                const double d = __longlong_as_double((long long)kd);
-                col[e] = j;
-                if (dist) dist[e] = d;
-                sorted_d[w][rank] = d;
-                if (disp) {
-                    const int na = (int)((kj >> 16) & 255) - 128, nb = (int)((kj >> 8) & 255) - 128,
-                              nc = (int)(kj & 255) - 128;
-                    double pj[3];
-                    P.get(j, pj);
-                    for (int k = 0; k < 3; ++k) {
-                        const double off = ((double)na * M.L[k] + (double)nb * M.L[3 + k]) + (double)nc * M.L[6 + k];
-                        disp[3 * e + k] = (pj[k] + off) - q[k];  // delta_r = p - q (neighbor_list.cpp:51)
-                    }
-                }
-            }
-        });
-        __builtin_amdgcn_wave_barrier();
-        // 3. RBF block: kept x nbins contiguous values starting at rs0 * nbins
-        if (rs.dtype != 0 && rbf) {
-            const int total = kept * rs.nbins;
-            if (rs.dtype == 1) write_rbf_block(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, sorted_d[w], rs);
-            else write_rbf_block(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sorted_d[w], rs);
-        }
-        __builtin_amdgcn_wave_barrier();
-    });
-}
-
-// ------------------------------------------------------------------------------------------
-// Kernel 3b: streaming emit from the rows the count pass stored (ROWS mode). A block covers
-// kQA atoms, whose edges and RBF rows are contiguous in the CSR: phase 1 places the kept rows
-// (col, dist, displacement) edge-parallel and keeps the distances in LDS; phase 2 writes the
-// block's whole RBF region as one flat stream of 16-byte stores.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float rbf_value_f32_fast(double d, int k, const RbfSpec& r) {
-    const double t = (double)k * r.dr - d;  // center - distance (edge_features.cpp:20-21)
-    const double x = ((-0.5 * (t * t)) * r.inv_sigma2) * 1.4426950408889634074;
-    const double n = rint(x);
-    const float e = __builtin_amdgcn_exp2f((float)(x - n));  // |x - n| <= 0.5
-    return __builtin_ldexpf(e, (int)n) * r.norm_f;
-}
-
-__global__ __launch_bounds__(kGraphBlock) void graph_emit_rows_kernel(
-    GraphLaunch g, const int32_t* __restrict__ counts, const int64_t* __restrict__ block_offsets,
-    const uint64_t* __restrict__ rows_d, const uint64_t* __restrict__ rows_j, int64_t* __restrict__ row_ptr,
-    int32_t* __restrict__ col, double* __restrict__ dist, double* __restrict__ disp, void* __restrict__ rbf,
-    RbfSpec rs) {
-    extern __shared__ double dl[];  // [kQA * K] distances of the block's edges, CSR order
-    __shared__ int64_t row_start[kQA + 1];
-    __shared__ int32_t cnt[kQA];
-    const int tid = threadIdx.x, lane = lane_id();
-    const int64_t g0 = (int64_t)blockIdx.x * kQA;
-    const int K = (int)g.kmax;
-    if (tid < kWave) {
-        const int64_t gi = g0 + lane;
-        const int64_t c = gi < g.num_atoms ? counts[gi] : 0;
-        const int64_t inc = wave_inclusive_sum(c);
-        const int64_t start = block_offsets[blockIdx.x] + inc - c;
-        row_start[lane] = start;
-        cnt[lane] = (int32_t)c;
         if (lane == kWave - 1) row_start[kQA] = start + c;
         if (gi < g.num_atoms) {
             row_ptr[gi] = start;
             if (gi == g.num_atoms - 1) row_ptr[g.num_atoms] = start + c;
         }
     }
+    // the count pass's hit masks of the block's atoms (staged one-image structures)
+    const int nwm = (stage_cap + 63) / 64;
+    if (g.mask)
+        for (int x = threadIdx.x; x < nq * nwm; x += kGraphBlock) {
+            const int a_ = x / nwm, wd = x - a_ * nwm;
+            mask_s[a_][wd] = g.mask[(g0 + a_) * kMaskWords + wd];
+        }
     __syncthreads();
     const int64_t e0 = row_start[0];
-    // phase 1: slot p = (atom a, rank r), r < K; stored rows are read in order (coalesced)
-    const float invK = 1.0f / (float)K;
-    for (int p = tid; p < kQA * K; p += kGraphBlock) {
-        int a = (int)((float)p * invK);
-        if (a * K > p) --a;
-        else if ((a + 1) * K <= p) ++a;
-        const int r = p - a * K;
-        const int64_t gi = g0 + a;
-        if (gi >= g.num_atoms || r >= cnt[a]) continue;
-        const uint64_t kd = rows_d[gi * K + r], kj = rows_j[gi * K + r];
-        const int64_t e = row_start[a] + r;
-        const double d = __longlong_as_double((long long)kd);
-        const int j = (int)(kj >> 24);
-        col[e] = j;
-        if (dist) dist[e] = d;
-        dl[e - e0] = d;
-        if (disp) {
-            const StructMeta& M = g.meta[g.atom_struct[gi]];
-            const int na = (int)((kj >> 16) & 255) - 128, nb = (int)((kj >> 8) & 255) - 128, nc = (int)(kj & 255) - 128;
-            const double* pj = g.pos + 3 * (M.first + j);
-            const double* q = g.pos + 3 * gi;
+    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
+        const int li = (int)(gi - M.first);
+        double q[3];
+        P.get(li, q);
+        // 1. compact the hits into the wave's LDS list (staged one-image structures: only the
+        // count pass's hits are evaluated)
+        int m = 0;
+        const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? lds(mask_s[t]) : nullptr;
+        search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double d2) {
+            const uint64_t bal = ballot(hit);
+            if (hit) {
+                const int slot = m + mask_prefix(bal);
+                if (slot < CAP) {
+                    key_d[w][slot] = sqrt(d2);  // neighbor_list.cpp:53
+                    key_j[w][slot] = pack_jimg(j, na, nb, nc);
+                }
+            }
+            m += __popcll(bal);
+        });
+        const int64_t rs0 = row_start[t];
+        const int kept = (int)(row_start[t + 1] - rs0);
+        if (m > CAP || kept != (m < K ? m : K)) {
+            if (lane == 0) atomicOr(error_flag, m > CAP ? kGErrCap : kGErrMismatch);
+            return;
+        }
+        wave_lds_sync();
+        // 2. rank by (distance, j, image) and place the kept rows
+        auto put = [&](int rank, double d, uint64_t kj) {
+            if (rank >= kept) return;
+            const int64_t e = rs0 + rank;
+            int j, na, nb, nc;
+            unpack_jimg(kj, j, na, nb, nc);
+            if constexpr (STREAM) {
+                dl[e - e0] = d;
+                colb[e - e0] = j;
+            } else {
+                sorted_d[w][rank] = d;
+                col[e] = j;
+                if (dist) dist[e] = d;
+            }
+            if (disp) {
+                double pj[3];
+                P.get(j, pj);
+                for (int k = 0; k < 3; ++k) {
+                    const double off = ((double)na * M.L[k] + (double)nb * M.L[3 + k]) + (double)nc * M.L[6 + k];
+                    disp[3 * e + k] = (pj[k] + off) - q[k];  // delta_r = p - q (neighbor_list.cpp:51)
+                }
+            }
+        };
+        if (m <= kWave) {
+#ifdef DGN_EMIT_NORANK
+            const int r = lane;  // A/B diagnostics only: rows in search order
+#else
+            const int r = rank_small(lds(key_d[w]), lds(key_j[w]), m, lds(claim[w]));
+#endif
+            if (lane < m) put(r, key_d[w][lane], key_j[w][lane]);
+        } else {
+            rank_large(lds(key_d[w]), lds(key_j[w]), m, put);
+        }
+        wave_lds_sync();
+        if constexpr (!STREAM) {
+            // 3. this atom's RBF block: kept x nbins contiguous values from rs0 * nbins
+            if (rs.dtype != 0 && rbf) {
+                const int total = kept * rs.nbins;
+                if (rs.dtype == 1)
+                    write_rbf_flat(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, lds(sorted_d[w]), rs, lane,
+                                   kWave);
+                else
+                    write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, lds(sorted_d[w]), rs, lane,
+                                   kWave);
+            }
+            wave_lds_sync();
+        }
+    });
+    if constexpr (STREAM) {
+        __syncthreads();
+        // the block's rows [e0, e1): columns and distances, coalesced
+        const int ne = (int)(row_start[kQA] - e0);
+        for (int i = threadIdx.x; i < ne; i += kGraphBlock) {
+            col[e0 + i] = colb[i];
+            if (dist) dist[e0 + i] = dl[i];
+        }
+        if (rs.dtype == 0 || !rbf) return;
+#ifdef DGN_EMIT_NORBF
+        return;  // A/B diagnostics only
+#endif
+        // the block's RBF region [e0 * nb, e1 * nb) as one flat stream
+        const int total = ne * rs.nbins;
+        if (rs.dtype == 1)
+            write_rbf_flat(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, total, dl, rs, threadIdx.x, kGraphBlock);
+        else
+            write_rbf_flat(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, total, dl, rs, threadIdx.x, kGraphBlock);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Betti distance pass with its own neighbour search: complex c = atom `first + c`, cloud row 0 =
+// pos_i, row k = pos_i + disp_k over every neighbour within rc (betti_features.cpp:67-73 with
+// NeighborList(rc, SIZE_MAX), :107). The persistence diagram and the 35 statistics do not depend
+// on the order of the cloud's rows (every distance depends only on its two points; the pairing
+// values of a filtration do not depend on its tie-breaking order), so the rows keep the search's
+// order instead of the sorted one. Writes the f32 lower triangle (MFMA Gram product) + npoints.
+// ------------------------------------------------------------------------------------------
+template <int CAP>
+__global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLaunch g, int64_t first, int64_t count,
+                                                                         int64_t tri_stride,
+                                                                         const int32_t* __restrict__ counts,
+                                                                         float* __restrict__ lower,
+                                                                         int32_t* __restrict__ npoints,
+                                                                         uint32_t* __restrict__ error_flag) {
+    __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
+    DGN_SEARCH_SMEM
+    __shared__ uint64_t key_j[kW][CAP];
+    __shared__ double sq_s[kW][CAP + 1 > kWave ? CAP + 1 : kWave];
+    __shared__ uint64_t mask_s[kQA][kMaskWords];
+    const StageView st = make_stage(stage_mem, kStage, offt_s);
+    const int w = threadIdx.x / kWave;
+    const int lane = lane_id();
+    const int64_t g0 = first + (int64_t)blockIdx.x * kQA;
+    const int nq = (int)(first + count - g0 < kQA ? first + count - g0 : kQA);
+    if (g.mask) {
+        for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock)
+            mask_s[x / kMaskWords][x % kMaskWords] = g.mask[g0 * kMaskWords + x];
+        __syncthreads();
+    }
+    for_block_atoms(g, st, first, first + count, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {
+        const int li = (int)(gi - M.first);
+        const int64_t c = gi - first;
+        double q[3];
+        P.get(li, q);
+        int m = 0;
+        const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? lds(mask_s[gi - g0]) : nullptr;
+        search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double) {
+            const uint64_t bal = ballot(hit);
+            if (hit) {
+                const int slot = m + mask_prefix(bal);
+                if (slot < CAP) key_j[w][slot] = pack_jimg(j, na, nb, nc);
+            }
+            m += __popcll(bal);
+        });
+        const int n = m + 1;
+        if (lane == 0) npoints[c] = n;
+        if (m > CAP || m != counts[gi]) {
+            if (lane == 0) atomicOr(error_flag, m > CAP ? kGErrCap : kGErrMismatch);
+            return;
+        }
+        wave_lds_sync();
+        // cloud row p: p = 0 the centre, else centre + ((p_j + offset) - centre)
+        auto point = [&](int p, double x[3]) __attribute__((always_inline)) {
+            if (p == 0) {
+                x[0] = q[0];
+                x[1] = q[1];
+                x[2] = q[2];
+                return;
+            }
+            int j, na, nb, nc;
+            unpack_jimg(key_j[w][p - 1], j, na, nb, nc);
+            double pj[3];
+            P.get(j, pj);
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const double off = ((double)na * M.L[k] + (double)nb * M.L[3 + k]) + (double)nc * M.L[6 + k];
-                disp[3 * e + k] = (pj[k] + off) - q[k];  // delta_r = p - q (neighbor_list.cpp:51)
+                x[k] = q[k] + ((pj[k] + off) - q[k]);  // betti_features.cpp:71: pos_i + disp_k
             }
+        };
+        float* L = lower + c * tri_stride;
+        if (n <= kWave) {
+            double px[3];
+            point(lane < n ? lane : n - 1, px);
+            gram_triangle_narrow(px, n, sq_s[w], L);
+        } else {
+            gram_triangle_wide(n, sq_s[w], L, point);
         }
-    }
-    if (rs.dtype == 0 || !rbf) return;
-    __syncthreads();
-    // phase 2: the block's RBF region [e0 * nb, e1 * nb) as one flat stream
-    const int nb = rs.nbins;
-    const int total = (int)(row_start[kQA] - e0) * nb;
-    auto split = [&](int f, int& le, int& k) {
-        le = (int)((float)f * rs.inv_nbins);
-        if (le * nb > f) --le;
-        else if ((le + 1) * nb <= f) ++le;
-        k = f - le * nb;
-    };
-    if (rs.dtype == 1) {
-        float* out = reinterpret_cast<float*>(rbf) + e0 * nb;
-        const int mis = (int)(((uintptr_t)out >> 2) & 3);
-        int head = mis ? 4 - mis : 0;
-        head = head < total ? head : total;
-        if (tid < head) {
-            int le, k;
-            split(tid, le, k);
-            out[tid] = rbf_value_f32_fast(dl[le], k, rs);
-        }
-        const int nvec = (total - head) >> 2;
-        for (int v = tid; v < nvec; v += kGraphBlock) {
-            const int f = head + 4 * v;
-            int le, k;
-            split(f, le, k);
-            float o[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                o[u] = rbf_value_f32_fast(dl[le], k, rs);
-                if (++k == nb) {
-                    k = 0;
-                    ++le;
-                }
-            }
-            // streaming (non-temporal) 16-byte store: the RBF block is written once, never re-read here
-            typedef float float4_t __attribute__((ext_vector_type(4)));
-            const float4_t ov = {o[0], o[1], o[2], o[3]};
-            __builtin_nontemporal_store(ov, reinterpret_cast<float4_t*>(out + f));
-        }
-        const int t0 = head + 4 * nvec;
-        if (t0 + tid < total) {
-            int le, k;
-            split(t0 + tid, le, k);
-            out[t0 + tid] = rbf_value_f32_fast(dl[le], k, rs);
-        }
-    } else {
-        double* out = reinterpret_cast<double*>(rbf) + e0 * nb;
-        const int head = ((((uintptr_t)out >> 3) & 1) && total > 0) ? 1 : 0;
-        if (tid < head) out[0] = rbf_value_f64(dl[0], 0, rs);
-        const int nvec = (total - head) >> 1;
-        for (int v = tid; v < nvec; v += kGraphBlock) {
-            const int f = head + 2 * v;
-            int le, k;
-            split(f, le, k);
-            double o[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                o[u] = rbf_value_f64(dl[le], k, rs);
-                if (++k == nb) {
-                    k = 0;
-                    ++le;
-                }
-            }
-            typedef double double2_t __attribute__((ext_vector_type(2)));
-            const double2_t ov = {o[0], o[1]};
-            __builtin_nontemporal_store(ov, reinterpret_cast<double2_t*>(out + f));
-        }
-        const int t0 = head + 2 * nvec;
-        if (t0 + tid < total) {
-            int le, k;
-            split(t0 + tid, le, k);
-            out[t0 + tid] = rbf_value_f64(dl[le], k, rs);
-        }
-    }
+    });
+}
+
+hipError_t launch_betti_dist_search(hipStream_t s, const GraphLaunch& g, int64_t first, int64_t count, int max_points,
+                                    int64_t tri_stride, const int32_t* counts, float* lower, int32_t* npoints,
+                                    uint32_t* error_flag) {
+    if (count <= 0) return hipSuccess;
+    const int64_t nb = graph_blocks(count);
+    if (max_points <= kWave)
+        hipLaunchKernelGGL(betti_dist_search_kernel<kWave>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, first,
+                           count, tri_stride, counts, lower, npoints, error_flag);
+    else
+        hipLaunchKernelGGL(betti_dist_search_kernel<kWideMaxPoints>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g,
+                           first, count, tri_stride, counts, lower, npoints, error_flag);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -659,7 +1165,7 @@ __global__ __launch_bounds__(256) void rbf_kernel(const double* __restrict__ d, 
             k = (int)(f / E);
             e = f - (int64_t)k * E;
         }
-        if (rs.dtype == 1) reinterpret_cast<float*>(out)[f] = rbf_value_f32(d[e], k, rs);
+        if (rs.dtype == 1) reinterpret_cast<float*>(out)[f] = rbf_f32((double)k * rs.dr - d[e], rs);
         else reinterpret_cast<double*>(out)[f] = rbf_value_f64(d[e], k, rs);
     }
 }
@@ -676,45 +1182,30 @@ hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& 
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
-hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset, int64_t B,
-                                  double rc, StructMeta* meta, int32_t* atom_struct) {
+hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const int64_t* atom_offset, const double* pos,
+                                  const int32_t* species, int64_t B, double rc, StructMeta* meta, int32_t* atom_struct,
+                                  int32_t* cell_start, double4* cell_pos, double* weight, uint32_t* error_flag) {
     if (B <= 0) return hipSuccess;
-    const int t = 128;
-    hipLaunchKernelGGL(prep_structures_kernel, dim3((unsigned)((B + t - 1) / t)), dim3(t), 0, s, lattice, atom_offset,
-                       B, rc, meta);
-    hipLaunchKernelGGL(map_atoms_kernel, dim3((unsigned)B), dim3(256), 0, s, atom_offset, atom_struct);
+    hipLaunchKernelGGL(prep_meta_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s, lattice, atom_offset, B,
+                       rc, meta);
+    hipLaunchKernelGGL(prep_atoms_kernel, dim3((unsigned)B), dim3(256), 0, s, meta, pos, species, atom_struct,
+                       cell_start, cell_pos, weight, error_flag);
     return hipGetLastError();
 }
 
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint64_t* block_aux, uint64_t* rows_d, uint64_t* rows_j) {
+                              uint64_t* block_aux, uint64_t* mask_out) {
     const int64_t nb = graph_blocks(g.num_atoms);
     if (nb <= 0) return hipSuccess;
-    if (rows_d)
-        hipLaunchKernelGGL(graph_count_kernel<true>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts,
-                           block_sums, block_aux, rows_d, rows_j);
-    else
-        hipLaunchKernelGGL(graph_count_kernel<false>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts,
-                           block_sums, block_aux, rows_d, rows_j);
-    return hipGetLastError();
-}
-
-hipError_t launch_graph_emit_rows(hipStream_t s, const GraphLaunch& g, const int32_t* counts,
-                                  const int64_t* block_offsets, const uint64_t* rows_d, const uint64_t* rows_j,
-                                  int64_t* row_ptr, int32_t* col, double* dist, double* disp, void* rbf,
-                                  const RbfSpec& rs) {
-    const int64_t nb = graph_blocks(g.num_atoms);
-    if (nb <= 0) return hipSuccess;
-    const size_t shmem = sizeof(double) * (size_t)kQA * (size_t)g.kmax;
-    hipLaunchKernelGGL(graph_emit_rows_kernel, dim3((unsigned)nb), dim3(kGraphBlock), shmem, s, g, counts,
-                       block_offsets, rows_d, rows_j, row_ptr, col, dist, disp, rbf, rs);
+    hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
+                       block_aux, mask_out);
     return hipGetLastError();
 }
 
 hipError_t launch_block_scan(hipStream_t s, int64_t* v, const uint64_t* aux, int64_t n, int64_t* total,
-                             uint32_t* max_candidates, unsigned long long* sum_sq) {
+                             uint32_t* max_candidates, unsigned long long* sum_sq, uint32_t* max_natoms) {
     hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, v, aux, n, total, max_candidates,
-                       sum_sq);
+                       sum_sq, max_natoms);
     return hipGetLastError();
 }
 
@@ -726,32 +1217,39 @@ int graph_emit_cap(uint32_t m) {
     return 0;
 }
 
-hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, const int32_t* counts,
+template <int CAP, bool STREAM>
+static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const int32_t* counts,
+                          const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
+                          void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
+    const int64_t nb = graph_blocks(g.num_atoms);
+    size_t shmem = (size_t)kStageBytesPerAtom * (size_t)stage;
+    if (STREAM) shmem += sizeof(double) * ((size_t)kQA * (size_t)g.kmax + 1) + sizeof(int32_t) * (size_t)kQA * (size_t)g.kmax;
+    hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)nb), dim3(kGraphBlock), shmem, s, g, stage,
+                       counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
+}
+
+hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
     const int64_t nb = graph_blocks(g.num_atoms);
     if (nb <= 0) return hipSuccess;
-    const dim3 grid((unsigned)nb), block(kGraphBlock);
+    const bool stream = g.kmax <= (uint64_t)kStreamMaxK;
+#define DGN_EMIT(C)                                                                                              \
+    case C:                                                                                                      \
+        if (stream) launch_emit_t<C, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, \
+                                           error_flag);                                                          \
+        else launch_emit_t<C, false>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,      \
+                                     error_flag);                                                                \
+        break;
     switch (cap) {
-        case 64:
-            hipLaunchKernelGGL(graph_emit_kernel<64>, grid, block, 0, s, g, counts, block_offsets, row_ptr, col,
-                               dist, disp, rbf, rs, error_flag);
-            break;
-        case 128:
-            hipLaunchKernelGGL(graph_emit_kernel<128>, grid, block, 0, s, g, counts, block_offsets, row_ptr, col,
-                               dist, disp, rbf, rs, error_flag);
-            break;
-        case 256:
-            hipLaunchKernelGGL(graph_emit_kernel<256>, grid, block, 0, s, g, counts, block_offsets, row_ptr, col,
-                               dist, disp, rbf, rs, error_flag);
-            break;
-        case 512:
-            hipLaunchKernelGGL(graph_emit_kernel<512>, grid, block, 0, s, g, counts, block_offsets, row_ptr, col,
-                               dist, disp, rbf, rs, error_flag);
-            break;
+        DGN_EMIT(64)
+        DGN_EMIT(128)
+        DGN_EMIT(256)
+        DGN_EMIT(512)
         default:
             return hipErrorInvalidValue;
     }
+#undef DGN_EMIT
     return hipGetLastError();
 }
 
