@@ -218,9 +218,12 @@ int take_emit_flag(dgn_ctx* c) {
     if (!c->emit_pending) return DGN_OK;
     c->emit_pending = false;
     const uint32_t f = c->host->emit_flag;
-    if (f & kGErrCap) return fail(c, DGN_ERR_INTERNAL, "graph emit: more candidates than the count pass reported");
-    if (f) return fail(c, DGN_ERR_INTERNAL, "graph emit disagreed with the count pass (flags " + std::to_string(f) + ")");
-    return DGN_OK;
+    if (!f) return DGN_OK;
+    std::string why;
+    if (f & kGErrCap) why += " [more candidates than the count pass reported]";
+    if (f & kGErrMismatch) why += " [kept rows differ from the count pass]";
+    if (f & kGErrMissedHit) why += " [a count-pass hit failed the exact test]";
+    return fail(c, DGN_ERR_INTERNAL, "graph emit disagreed with the count pass (flags " + std::to_string(f) + ")" + why);
 }
 
 GraphLaunch graph_launch(GraphWork& W, const dgn_batch* b, double rc, double eps, uint64_t kmax, bool use_mask) {

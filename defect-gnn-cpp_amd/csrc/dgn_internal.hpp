@@ -21,6 +21,7 @@ constexpr int kMaskWords = kStage / 64;   // hit-mask words per query atom (stag
 constexpr uint32_t kGErrCap = 1u << 0;       // more candidates than the emit capacity
 constexpr uint32_t kGErrMismatch = 1u << 1;  // emit / Betti search disagrees with the count pass
 constexpr uint32_t kGErrFar = 1u << 2;       // a position more than 500 cells away from the origin
+constexpr uint32_t kGErrMissedHit = 1u << 3; // a count-pass hit failed the emit's exact test
 
 struct GraphLaunch {
     const StructMeta* meta;

@@ -505,6 +505,21 @@ __device__ __forceinline__ FromMask load_mask(const DGN_LDS uint64_t* m, int nat
     return {(uint32_t)w, (uint32_t)(w >> 32)};
 }
 
+// The count pass's hits of one query as atom indices, ascending, in hit[0 .. m) (per-wave LDS):
+// word t of the mask is tile t's hit ballot, so lane j's slot is the hits before it (popcounts of
+// the earlier words + mbcnt). Returns m.
+__device__ __forceinline__ int collect_mask_hits(const DGN_LDS uint64_t* mask, int natoms, DGN_LDS uint32_t* hit) {
+    const int lane = lane_id();
+    int m = 0;
+    for (int t = 0; 64 * t < natoms; ++t) {
+        const uint64_t word = mask[t];  // broadcast read
+        if ((word >> lane) & 1ull) hit[m + mask_prefix(word)] = (uint32_t)(64 * t + lane);
+        m += __popcll(word);
+    }
+    wave_lds_sync();
+    return m;
+}
+
 // (2) cell list (structures above kStage atoms, one image per axis)
 template <class Visit>
 __device__ __forceinline__ void search_cells(const GraphLaunch& g, const StructMeta& M, int64_t b, const double q[3],
@@ -903,35 +918,137 @@ __device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, c
 }
 
 // ------------------------------------------------------------------------------------------
+// Block RBF stream (STREAM emit): the block's edges are processed EP at a time per wave; lane =
+// (edge, segment of h bins). With t0 = k0 dr - d the segment start's offset from the centre,
+//   g_{k0+i} = norm exp(-0.5 (t0 + i dr)^2 / s^2) = G_i C_i,   G_i = g_{k0} B^i,
+//   B = exp(-t0 dr / s^2),   C_i = exp(-0.5 i^2 dr^2 / s^2)  (table),
+// so each value costs two f64 multiplies (G_{i+1} = G_i B, G_i C_i) after two exps per lane; the
+// running product carries i + 3 roundings (<= 1e-14 relative for i <= 100, far inside the f64
+// path's 1e-13 and the f32 path's 1e-6). Values go to a per-wave LDS buffer laid out like the
+// output (shifted to the output's 16-byte phase) and leave as non-temporal 16-byte stores.
+// ------------------------------------------------------------------------------------------
+struct RbfStreamGeom {
+    int ep, seg, h;  // edges per pass, lanes per edge, bins per lane
+};
+__host__ __device__ inline RbfStreamGeom rbf_stream_geom(int nb, int elem) {
+    constexpr int kBufBytes = 4096;  // per wave
+    int ep = kBufBytes / (nb * elem);
+    ep = ep < 1 ? 1 : (ep > kWave ? kWave : ep);
+    int sg = kWave / ep;
+    sg = sg > nb ? nb : sg;
+    return {ep, sg, (nb + sg - 1) / sg};
+}
+template <typename T>
+__device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, const DGN_LDS double* dl,
+                                                const DGN_LDS double* ctab, DGN_LDS T* buf, const RbfSpec& rs,
+                                                const RbfStreamGeom gm, int w) {
+    constexpr int V = 16 / sizeof(T);
+    const int lane = lane_id();
+    const int nb = rs.nbins;
+    const int le = lane / gm.seg, sgi = lane - le * gm.seg;
+    const int k0 = sgi * gm.h;
+    const int cnt0 = nb - k0 < gm.h ? nb - k0 : gm.h;
+    for (int e = w * gm.ep; e < ne; e += kW * gm.ep) {
+        const int nedge = ne - e < gm.ep ? ne - e : gm.ep;
+        T* o = out + (int64_t)e * nb;
+        const int phase = (int)(((uintptr_t)o / sizeof(T)) & (V - 1));  // o - phase is 16-byte aligned
+        if (le < nedge && cnt0 > 0) {
+            const double d = dl[e + le];
+            const double t0 = (double)k0 * rs.dr - d;
+            const double s = rs.inv_sigma2;
+            double G = rs.norm * exp(-0.5 * (t0 * t0) * s);
+            const double B = exp(-(t0 * rs.dr) * s);
+            DGN_LDS T* dst = buf + phase + le * nb + k0;
+            for (int i = 0; i < cnt0; ++i) {
+                dst[i] = (T)(G * ctab[i]);
+                G *= B;
+            }
+        }
+        wave_lds_sync();
+        // stream buf[phase, phase + nedge * nb) -> o[0, nedge * nb): lanes cover 16-byte units
+        const int total = nedge * nb + phase;  // in units of T from the aligned base o - phase
+        const int nvec = (total + V - 1) / V;
+        for (int v = lane; v < nvec; v += kWave) {
+            const int f = V * v;
+            if (f >= phase && f + V <= total) {
+                typedef T vec_t __attribute__((ext_vector_type(V)));
+                const vec_t val = *reinterpret_cast<const DGN_LDS vec_t*>(buf + f);
+                __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(o - phase + f));
+            } else {
+                for (int u = 0; u < V; ++u)
+                    if (f + u >= phase && f + u < total) (o - phase)[f + u] = buf[f + u];
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Kernel 3: fused emit. Per atom (one wave): search, compact the hits into LDS, rank, write the
 // kept rows (col, distance, displacement). STREAM (max_neighbors <= kStreamMaxK): the kept
 // distances of the block's edges are kept in LDS and, after the block's atoms are done, its whole
 // RBF region (contiguous in the CSR) is written as one flat stream by all 256 threads; otherwise
 // each wave writes its atom's RBF block.
 // ------------------------------------------------------------------------------------------
+// Dynamic LDS of the emit (bytes): region A (search phase: stage, hit lists, hit masks) is dead
+// once the block's atoms are placed and is reused as region B (the per-wave RBF buffers); then
+// the block's rows (distances, columns) and the RBF C table, which live to the end.
+struct EmitLayout {
+    int stage, keyd, keyj, mask, sorted, rbf, dl, colb, ctab, total;
+    RbfStreamGeom gm;
+};
+__host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool stream, int K, int nb, int elem,
+                                                  int nwm) {
+    EmitLayout l{};
+    int o = 0;
+    auto take = [&](int bytes) {
+        const int at = o;
+        o += (bytes + 15) / 16 * 16;
+        return at;
+    };
+    l.stage = take(stage_cap * kStageBytesPerAtom);
+    l.keyd = take(kW * cap * 8);
+    l.keyj = take(kW * cap * 8);
+    l.mask = take(kQA * nwm * 8);
+    l.sorted = take(stream ? 0 : kW * (cap + 1) * 8);
+    const int a_end = o;
+    l.gm = rbf_stream_geom(nb > 0 ? nb : 1, elem > 0 ? elem : 4);
+    const int b_bytes = (stream && nb > 0) ? kW * ((l.gm.ep * nb + 16 / (elem > 0 ? elem : 4)) * (elem > 0 ? elem : 4) + 16) : 0;
+    l.rbf = 0;
+    o = a_end > b_bytes ? a_end : (b_bytes + 15) / 16 * 16;
+    l.dl = take(stream ? (kQA * K + 1) * 8 : 0);
+    l.colb = take(stream ? kQA * K * 4 : 0);
+    l.ctab = take(stream ? (l.gm.h + 1) * 8 : 0);
+    l.total = o;
+    return l;
+}
+
 template <int CAP, bool STREAM>
-__global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, int stage_cap,
+__global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, int stage_cap, int nwm,
                                                                   const int32_t* __restrict__ counts,
                                                                   const int64_t* __restrict__ block_offsets,
                                                                   int64_t* __restrict__ row_ptr,
                                                                   int32_t* __restrict__ col, double* __restrict__ dist,
                                                                   double* __restrict__ disp, void* __restrict__ rbf,
                                                                   RbfSpec rs, uint32_t* __restrict__ error_flag) {
-    // dynamic: the stage [stage_cap atoms]; STREAM: the block's edge distances [kQA * K + 1] and
-    // columns [kQA * K] (written to HBM once the block's atoms are done, coalesced)
     extern __shared__ double dyn[];
-    DGN_SEARCH_SMEM
-    __shared__ double key_d[kW][CAP];
-    __shared__ uint64_t key_j[kW][CAP];
-    __shared__ double sorted_d[kW][STREAM ? 1 : CAP + 1];
+    __shared__ double4 offt_s[125];
+    __shared__ uint32_t ring[kW][kRing];
     __shared__ uint8_t claim[kW][kWave];
     __shared__ int64_t row_start[kQA + 1];
-    __shared__ uint64_t mask_s[kQA][kMaskWords];
-    const StageView st = make_stage(dyn, stage_cap, offt_s);
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
-    DGN_LDS double* dl = lds(dyn) + stage_cap * kStageBytesPerAtom / 8;
-    DGN_LDS int32_t* colb = reinterpret_cast<DGN_LDS int32_t*>(dl + (STREAM ? kQA * K + 1 : 0));
-    const int w = threadIdx.x / kWave;
+    const int elem = rs.dtype == 2 ? 8 : 4;
+    const EmitLayout ly = emit_layout(stage_cap, CAP, STREAM, STREAM ? K : 0, rs.dtype ? rs.nbins : 0, elem, nwm);
+    DGN_LDS uint8_t* base = reinterpret_cast<DGN_LDS uint8_t*>(lds(dyn));
+    const StageView st = make_stage(reinterpret_cast<double*>(dyn) + ly.stage / 8, stage_cap, offt_s);
+    DGN_LDS double* key_d = reinterpret_cast<DGN_LDS double*>(base + ly.keyd);
+    DGN_LDS uint64_t* key_j = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.keyj);
+    DGN_LDS uint64_t* mask_s = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.mask);
+    DGN_LDS double* sorted_d = reinterpret_cast<DGN_LDS double*>(base + ly.sorted);
+    DGN_LDS double* dl = reinterpret_cast<DGN_LDS double*>(base + ly.dl);
+    DGN_LDS int32_t* colb = reinterpret_cast<DGN_LDS int32_t*>(base + ly.colb);
+    DGN_LDS double* ctab = reinterpret_cast<DGN_LDS double*>(base + ly.ctab);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int lane = lane_id();
     const int64_t g0 = (int64_t)blockIdx.x * kQA;
     const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
@@ -950,51 +1067,95 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         }
     }
     // the count pass's hit masks of the block's atoms (staged one-image structures)
-    const int nwm = (stage_cap + 63) / 64;
     if (g.mask)
         for (int x = threadIdx.x; x < nq * nwm; x += kGraphBlock) {
             const int a_ = x / nwm, wd = x - a_ * nwm;
-            mask_s[a_][wd] = g.mask[(g0 + a_) * kMaskWords + wd];
+            mask_s[x] = g.mask[(g0 + a_) * kMaskWords + wd];
+        }
+    // C_i = exp(-0.5 i^2 dr^2 / s^2) of the RBF stream
+    if (STREAM && rs.dtype != 0)
+        for (int i = threadIdx.x; i <= ly.gm.h; i += kGraphBlock) {
+            const double x = (double)i * rs.dr;
+            ctab[i] = exp(-0.5 * (x * x) * rs.inv_sigma2);
         }
     __syncthreads();
     const int64_t e0 = row_start[0];
-    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
+    DGN_LDS double* kd = key_d + w * CAP;
+    DGN_LDS uint64_t* kj = key_j + w * CAP;
+    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
+                                               __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
         // 1. compact the hits into the wave's LDS list (staged one-image structures: only the
         // count pass's hits are evaluated)
         int m = 0;
-        const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? lds(mask_s[t]) : nullptr;
-        search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double d2) {
-            const uint64_t bal = ballot(hit);
-            if (hit) {
-                const int slot = m + mask_prefix(bal);
-                if (slot < CAP) {
-                    key_d[w][slot] = sqrt(d2);  // neighbor_list.cpp:53
-                    key_j[w][slot] = pack_jimg(j, na, nb, nc);
+        bool fast = false;
+        const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? mask_s + t * nwm : nullptr;
+        if (mk) {
+            // fast path: at most 64 hits, one lane each, straight from the count pass's mask
+            const int mh = collect_mask_hits(mk, M.natoms, lds(ring[w]));
+            if (mh <= kWave) {
+                fast = true;
+                m = mh;
+                bool ok = true;
+                if (lane < m) {
+                    const int j = (int)ring[w][lane];
+                    int n[3];
+                    bool inr;
+                    const double d2 = exact_one(P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    ok = inr && d2 < g.rc2;
+                    kd[lane] = sqrt(d2);  // neighbor_list.cpp:53
+                    kj[lane] = pack_jimg(j, n[0], n[1], n[2]);
+#ifdef DGN_EMIT_DEBUG
+                    if (!ok)
+                        printf("fast miss gi=%ld li=%d j=%d m=%d n=%d,%d,%d inr=%d d2=%.17g rc2=%.17g fq=%x,%x,%x,%x fj=%x,%x,%x,%x\n",
+                               (long)gi, li, j, m, n[0], n[1], n[2], (int)inr, d2, g.rc2, P.st.fx[li].x, P.st.fx[li].y,
+                               P.st.fx[li].z, P.st.fx[li].w, P.st.fx[j].x, P.st.fx[j].y, P.st.fx[j].z, P.st.fx[j].w);
+#endif
+                }
+                if (ballot(!ok)) {
+                    if (lane == 0) atomicOr(error_flag, kGErrMissedHit);
+                    return;
                 }
             }
-            m += __popcll(bal);
-        });
+        }
+        if (!fast)
+            search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double d2) {
+                const uint64_t bal = ballot(hit);
+                if (hit) {
+                    const int slot = m + mask_prefix(bal);
+                    if (slot < CAP) {
+                        kd[slot] = sqrt(d2);  // neighbor_list.cpp:53
+                        kj[slot] = pack_jimg(j, na, nb, nc);
+                    }
+                }
+                m += __popcll(bal);
+            });
         const int64_t rs0 = row_start[t];
         const int kept = (int)(row_start[t + 1] - rs0);
         if (m > CAP || kept != (m < K ? m : K)) {
             if (lane == 0) atomicOr(error_flag, m > CAP ? kGErrCap : kGErrMismatch);
+#ifdef DGN_EMIT_DEBUG
+            if (lane == 0)
+                printf("emit mismatch gi=%ld b=%ld t=%d m=%d kept=%d fast=%d natoms=%d staged=%d one=%d w0=%lx w1=%lx\n",
+                       (long)gi, (long)b, t, m, kept, (int)fast, M.natoms, (int)P.staged, M.one,
+                       (unsigned long)(mk ? mk[0] : 0), (unsigned long)(mk ? mk[1] : 0));
+#endif
             return;
         }
         wave_lds_sync();
         // 2. rank by (distance, j, image) and place the kept rows
-        auto put = [&](int rank, double d, uint64_t kj) {
+        auto put = [&](int rank, double d, uint64_t key) __attribute__((always_inline)) {
             if (rank >= kept) return;
             const int64_t e = rs0 + rank;
             int j, na, nb, nc;
-            unpack_jimg(kj, j, na, nb, nc);
+            unpack_jimg(key, j, na, nb, nc);
             if constexpr (STREAM) {
                 dl[e - e0] = d;
                 colb[e - e0] = j;
             } else {
-                sorted_d[w][rank] = d;
+                sorted_d[w * (CAP + 1) + rank] = d;
                 col[e] = j;
                 if (dist) dist[e] = d;
             }
@@ -1011,11 +1172,11 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 #ifdef DGN_EMIT_NORANK
             const int r = lane;  // A/B diagnostics only: rows in search order
 #else
-            const int r = rank_small(lds(key_d[w]), lds(key_j[w]), m, lds(claim[w]));
+            const int r = rank_small(kd, kj, m, lds(claim[w]));
 #endif
-            if (lane < m) put(r, key_d[w][lane], key_j[w][lane]);
+            if (lane < m) put(r, kd[lane], kj[lane]);
         } else {
-            rank_large(lds(key_d[w]), lds(key_j[w]), m, put);
+            rank_large(kd, kj, m, put);
         }
         wave_lds_sync();
         if constexpr (!STREAM) {
@@ -1023,17 +1184,17 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             if (rs.dtype != 0 && rbf) {
                 const int total = kept * rs.nbins;
                 if (rs.dtype == 1)
-                    write_rbf_flat(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, lds(sorted_d[w]), rs, lane,
-                                   kWave);
+                    write_rbf_flat(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, sorted_d + w * (CAP + 1), rs,
+                                   lane, kWave);
                 else
-                    write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, lds(sorted_d[w]), rs, lane,
-                                   kWave);
+                    write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sorted_d + w * (CAP + 1), rs,
+                                   lane, kWave);
             }
             wave_lds_sync();
         }
     });
     if constexpr (STREAM) {
-        __syncthreads();
+        __syncthreads();  // region A (stage, hit lists) is dead from here: region B reuses it
         // the block's rows [e0, e1): columns and distances, coalesced
         const int ne = (int)(row_start[kQA] - e0);
         for (int i = threadIdx.x; i < ne; i += kGraphBlock) {
@@ -1044,12 +1205,13 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 #ifdef DGN_EMIT_NORBF
         return;  // A/B diagnostics only
 #endif
-        // the block's RBF region [e0 * nb, e1 * nb) as one flat stream
-        const int total = ne * rs.nbins;
+        const int wbytes = ((ly.gm.ep * rs.nbins + 16 / elem) * elem + 16);
         if (rs.dtype == 1)
-            write_rbf_flat(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, total, dl, rs, threadIdx.x, kGraphBlock);
+            rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
+                            reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * wbytes), rs, ly.gm, w);
         else
-            write_rbf_flat(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, total, dl, rs, threadIdx.x, kGraphBlock);
+            rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
+                            reinterpret_cast<DGN_LDS double*>(base + ly.rbf + w * wbytes), rs, ly.gm, w);
     }
 }
 
@@ -1089,15 +1251,38 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
         double q[3];
         P.get(li, q);
         int m = 0;
+        bool fast = false;
         const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? lds(mask_s[gi - g0]) : nullptr;
-        search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double) {
-            const uint64_t bal = ballot(hit);
-            if (hit) {
-                const int slot = m + mask_prefix(bal);
-                if (slot < CAP) key_j[w][slot] = pack_jimg(j, na, nb, nc);
+        if (mk) {
+            // at most 63 hits: the count pass's mask, the images from the fixed-point coordinates
+            const int mh = collect_mask_hits(mk, M.natoms, lds(ring[w]));
+            if (mh < kWave) {
+                fast = true;
+                m = mh;
+                bool ok = true;
+                if (lane < m) {
+                    const int j = (int)ring[w][lane];
+                    int n[3];
+                    bool inr;
+                    const double d2 = exact_one(P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    ok = inr && d2 < g.rc2;
+                    key_j[w][lane] = pack_jimg(j, n[0], n[1], n[2]);
+                }
+                if (ballot(!ok)) {
+                    if (lane == 0) atomicOr(error_flag, kGErrMismatch);
+                    return;
+                }
             }
-            m += __popcll(bal);
-        });
+        }
+        if (!fast)
+            search(g, M, b, P, q, li, lds(ring[w]), mk, [&](bool hit, int j, int na, int nb, int nc, double) {
+                const uint64_t bal = ballot(hit);
+                if (hit) {
+                    const int slot = m + mask_prefix(bal);
+                    if (slot < CAP) key_j[w][slot] = pack_jimg(j, na, nb, nc);
+                }
+                m += __popcll(bal);
+            });
         const int n = m + 1;
         if (lane == 0) npoints[c] = n;
         if (m > CAP || m != counts[gi]) {
@@ -1222,10 +1407,11 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
                           const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
                           void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
     const int64_t nb = graph_blocks(g.num_atoms);
-    size_t shmem = (size_t)kStageBytesPerAtom * (size_t)stage;
-    if (STREAM) shmem += sizeof(double) * ((size_t)kQA * (size_t)g.kmax + 1) + sizeof(int32_t) * (size_t)kQA * (size_t)g.kmax;
-    hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)nb), dim3(kGraphBlock), shmem, s, g, stage,
-                       counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
+    const int nwm = (stage + 63) / 64;
+    const int K = STREAM ? (int)g.kmax : 0;
+    const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
+    hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)nb), dim3(kGraphBlock), (size_t)ly.total, s, g,
+                       stage, nwm, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
 }
 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,

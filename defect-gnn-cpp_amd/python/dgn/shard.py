@@ -28,6 +28,52 @@ def merge_csr(shards: list[dict]) -> dict:
     return out
 
 
+class Shard:
+    """One rank's share of a synthetic bench workload (bench.py and the multi-process tests):
+    structures [rank*B, (rank+1)*B) of `synth_batch(kind, m)`, inputs resident on `dev`, output
+    buffers allocated once; `step` runs the whole hot path over the shard through the C ABI."""
+
+    def __init__(self, dgn, abi, kind: str, m: int, structures: int, rank: int, dev):
+        import torch
+        self.dgn, self.abi, self.dev = dgn, abi, dev
+        self.B = int(structures)
+        self.host = dgn.synth_batch(kind, m, self.B, first_id=rank * self.B)
+        self.batch = {k: torch.from_numpy(v).to(dev) for k, v in self.host.items()}
+        self.A = int(self.host["positions"].shape[0])
+        self.n_atoms = self.A // self.B
+        self.E = 0
+        self.out = {}
+
+    def alloc_graph(self, ctx, gp, nbins: int, rbf_dtype) -> int:
+        import torch
+        self.E = ctx.dev_graph_count(self.batch, gp)
+        e = max(self.E, 1)
+        self.out.update(row_ptr=torch.empty(self.A + 1, dtype=torch.int64, device=self.dev),
+                        col=torch.empty(e, dtype=torch.int32, device=self.dev),
+                        dist=torch.empty(e, dtype=torch.float64, device=self.dev),
+                        rbf=torch.empty((e, nbins), dtype=rbf_dtype, device=self.dev))
+        return self.E
+
+    def alloc_betti(self):
+        import torch
+        self.out.update(feat=torch.empty((self.A, 35), dtype=torch.float64, device=self.dev),
+                        counts=torch.empty((self.A, 4), dtype=torch.int32, device=self.dev))
+
+    def step(self, ctx, gp, betti_rc: float, betti: bool = True, graph: bool = True):
+        if graph:
+            e = ctx.dev_graph_count(self.batch, gp)
+            if e != self.E:
+                raise RuntimeError(f"edge count changed between steps: {e} != {self.E}")
+            o = self.out
+            ctx.dev_graph_emit(self.batch, gp, o["row_ptr"], o["col"], o["dist"], None, o["rbf"])
+        if betti:
+            ctx.dev_betti(self.batch, betti_rc, self.out["feat"], self.out["counts"])
+
+    def results(self) -> dict:
+        """Host copies of every output buffer (row_ptr local to the shard)."""
+        return {k: v.cpu().numpy() for k, v in self.out.items()}
+
+
 def gather_csr(local: dict, dst: int = 0, group=None):
     """Gather every rank's CSR dict to rank `dst` (torch.distributed, any backend; objects are
     sent as numpy arrays). Returns the merged CSR on dst, None elsewhere."""

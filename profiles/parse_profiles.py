@@ -1,6 +1,7 @@
 """Fold one round's rocprofv3 output (profiles/collect.sh) into committed summaries:
   profiles/<round>_kernel_stats.csv   rocprofv3 --stats table of the default bench
-  profiles/<round>_summary.json       per-kernel avg duration + PMC HBM bytes per graph-emit launch
+  profiles/<round>_summary.json       per-kernel avg duration + PMC HBM bytes per launch of every
+                                      neighbour-path kernel (prep, count, scan, emit) and their sum
   profiles/traffic_latest.json        what bench.py reads for roofline.traffic
 HBM bytes per launch = 2 x FETCH_SIZE (gfx950 tallies 128-B read requests at 64 B,
 MI355X_MICROARCH.md "HBM") + WRITE_SIZE (exact for wide streaming stores); FETCH/WRITE_SIZE are in KB.
@@ -13,6 +14,8 @@ import os
 import shutil
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# the neighbour + RBF path (bench.py roofline): prep_structures = prep_meta + prep_atoms
+PATH_KERNELS = ("prep_meta_kernel", "prep_atoms_kernel", "graph_count_kernel", "block_scan_kernel", "graph_emit_kernel")
 
 
 def find(d, pattern):
@@ -51,27 +54,29 @@ def main():
     fetch = find(os.path.join(a.dir, "fetch"), "*counter_collection.csv")
     write = find(os.path.join(a.dir, "write"), "*counter_collection.csv")
     if fetch and write:
-        fv = pmc_per_launch(fetch, "graph_emit", "FETCH_SIZE")
-        wv = pmc_per_launch(write, "graph_emit", "WRITE_SIZE")
-        if fv and wv:
-            f_kb = sum(fv) / len(fv)
-            w_kb = sum(wv) / len(wv)
-            hbm = 2 * f_kb * 1024 + w_kb * 1024
+        per_kernel = {}
+        for k in PATH_KERNELS:
+            fv = pmc_per_launch(fetch, k, "FETCH_SIZE")
+            wv = pmc_per_launch(write, k, "WRITE_SIZE")
+            if fv and wv:
+                f_kb = sum(fv) / len(fv)
+                w_kb = sum(wv) / len(wv)
+                per_kernel[k] = {"launches": len(fv), "fetch_kb": f_kb, "write_kb": w_kb,
+                                 "hbm_bytes_per_launch": 2 * f_kb * 1024 + w_kb * 1024}
+        if "graph_emit_kernel" in per_kernel:
             gb = summary.get("fetch_bench", {})
             cfg = gb.get("config", {})
-            emit = summary.get("trace_bench", {}).get("roofline") or {}
-            key = None
-            if cfg:
-                # must match bench.py's workload_key for the default run
-                key = "fcc4x%d_rc5.0_k20_nb50" % cfg.get("structures_per_gpu", 0)
-            summary["graph_emit_pmc"] = {"launches": len(fv), "fetch_kb": f_kb, "write_kb": w_kb,
-                                         "hbm_bytes_per_launch": hbm,
-                                         "algorithmic_bytes_per_launch": emit.get("algorithmic_bytes_per_launch"),
+            roof = summary.get("trace_bench", {}).get("roofline") or {}
+            # must match bench.py's workload_key for the default run
+            key = "fcc4x%d_rc5.0_k20_nb50" % cfg.get("structures_per_gpu", 0) if cfg else None
+            path = sum(v["hbm_bytes_per_launch"] for v in per_kernel.values())
+            summary["graph_path_pmc"] = {"per_kernel": per_kernel, "hbm_bytes_per_path": path,
+                                         "algorithmic_bytes_per_path": roof.get("algorithmic_bytes_per_launch"),
                                          "workload_key": key}
             with open(os.path.join(HERE, "traffic_latest.json"), "w") as f:
-                json.dump({"round": a.round, "workload_key": key, "hbm_bytes_per_launch": hbm,
-                           "fetch_kb_x2": 2 * f_kb, "write_kb": w_kb,
-                           "source": f"profiles/{a.round}_summary.json"}, f, indent=1)
+                json.dump({"round": a.round, "workload_key": key, "hbm_bytes_per_path": path,
+                           "hbm_bytes_per_emit": per_kernel["graph_emit_kernel"]["hbm_bytes_per_launch"],
+                           "per_kernel": per_kernel, "source": f"profiles/{a.round}_summary.json"}, f, indent=1)
     with open(os.path.join(HERE, f"{a.round}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "kernel_stats"}, indent=1)[:4000])

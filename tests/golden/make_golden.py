@@ -56,7 +56,7 @@ def betti_ref(lat, pos, species, rc):
 
 def main():
     assert O.ref_available(), "build oracle/_ref first (make -C oracle)"
-    # (i) POSCARs: inputs + CSR at rc=5, K=12/20, RBF (rc=5, dr=0.1), Betti at rc=5
+    # (i) POSCARs: inputs + CSR at rc=5, K=12/20, RBF (rc=5, dr=0.1) of 1 / 741, Betti at rc=5 of all
     poscar = {}
     for path in sorted(glob.glob(os.path.join(REF_POSCARS, "*.vasp"))):
         name = os.path.basename(path)[:-5]
@@ -72,7 +72,9 @@ def main():
             if name in ("1", "741"):
                 poscar[f"{name}/k{k}/rbf"] = np.stack([O.gaussian_rbf(d, 5.0, 0.1) for d in nl["dist"]]).astype(
                     np.float64)
-        if name in ("1", "741"):
+        # Betti at 5 A for all nine files: the (birth, death) multisets (hence the features) do not
+        # depend on how distance ties are ordered, so the tied 1046* / *_1 / *_2 files pin too
+        if True:
             f, c = betti_ref(lat, pos, sp, 5.0)
             poscar[f"{name}/betti5/features"] = f
             poscar[f"{name}/betti5/counts"] = c

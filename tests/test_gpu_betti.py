@@ -63,7 +63,7 @@ def test_sc64_fixture(ctx, s):
     np.testing.assert_allclose(f, fx[f"{s}/features"], rtol=FEAT_RTOL, atol=FEAT_ATOL)
 
 
-@pytest.mark.parametrize("name", ["1", "741"])
+@pytest.mark.parametrize("name", ["1", "1046", "1046_1", "1046_2", "1_1", "1_2", "741", "741_1", "741_2"])
 def test_poscar_fixture(ctx, name):
     fx = np.load(os.path.join(GOLDEN, "poscar_rc5.npz"))
     pos = fx[f"{name}/positions"]

@@ -128,3 +128,31 @@ def test_rbf_of_given_distances(ctx, layout):
         ref = np.stack([O.gaussian_rbf(x, 10.0, 0.1) for x in d])
         assert out.shape == ref.shape
         assert np.max(np.abs(out - ref) / ref) < tol
+
+
+def test_device_count_emit_full_shard(ctx):
+    """The bench's device-level path (dgn_dev_graph_count -> dgn_dev_graph_emit on torch tensors)
+    at the full config-4 shard size, twice: the emit's deferred consistency flag must stay clear
+    and sampled structures must match the oracle bit for bit."""
+    import torch
+    B = 8192
+    host = dgn.synth_batch("fcc", 4, B)
+    batch = {k: torch.from_numpy(v).cuda() for k, v in host.items()}
+    gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F32)
+    A = host["positions"].shape[0]
+    for _ in range(2):
+        E = ctx.dev_graph_count(batch, gp)
+        rp = torch.empty(A + 1, dtype=torch.int64, device="cuda")
+        col = torch.empty(E, dtype=torch.int32, device="cuda")
+        dist = torch.empty(E, dtype=torch.float64, device="cuda")
+        rbf = torch.empty((E, 50), dtype=torch.float32, device="cuda")
+        ctx.dev_graph_emit(batch, gp, rp, col, dist, None, rbf)
+        ctx.synchronize()  # raises on a count/emit disagreement
+    rp, col, dist, rbf = rp.cpu().numpy(), col.cpu().numpy(), dist.cpu().numpy(), rbf.cpu().numpy()
+    n = 256
+    for s in (0, 1, 4095, B - 1):
+        nl = O.neighbor_list(host["lattice"][s], host["positions"][s * n:(s + 1) * n], 5.0, 20)
+        a, b = rp[s * n], rp[(s + 1) * n]
+        assert np.array_equal(rp[s * n:(s + 1) * n + 1] - a, nl["row_ptr"])
+        assert np.array_equal(col[a:b], nl["col"]) and np.array_equal(dist[a:b], nl["dist"])
+        check_rbf(rbf[a:b], nl["dist"], 5.0, 0.1)

@@ -77,7 +77,7 @@ def test_sc64_betti_against_fixture(sc64, s):
             assert np.array_equal(r[d], sc64[f"{s}/pairs{a}/{d}"])
 
 
-@pytest.mark.parametrize("name", ["1", "741"])
+@pytest.mark.parametrize("name", ["1", "1046", "1046_1", "1046_2", "1_1", "1_2", "741", "741_1", "741_2"])
 def test_poscar_betti_against_fixture(poscar, name):
     f, c = O.structure_betti(poscar[f"{name}/lattice"], poscar[f"{name}/positions"], poscar[f"{name}/species"], 5.0)
     assert np.array_equal(c, poscar[f"{name}/betti5/counts"])
