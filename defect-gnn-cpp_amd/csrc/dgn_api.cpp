@@ -118,6 +118,7 @@ struct dgn_ctx {
     int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's tables were initialised for
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
+    DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
 #ifdef DGN_PHASE_TIMING
     DevBuf phase;
     unsigned long long phase_host[32] = {0};
@@ -320,10 +321,16 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     const double bytes = 24 * A + 72 * B + 4 * A + 8 * (A + 1) + E * (4 + (dist ? 8 : 0)) + (disp ? 24 * E : 0) +
                          (rbf ? E * rs.nbins * rbf_bytes : 0);
     const int stage = (int)std::min<uint32_t>(W.max_natoms, (uint32_t)kStage);
+    // the block RBF stream re-reads the block's distance rows
+    double* dist_rows = dist;
+    if (!dist && rbf && rs.dtype != DGN_NONE) {
+        HIP_TRY(c, c->dist_scratch.ensure((size_t)std::max<int64_t>(W.edges, 1) * sizeof(double)));
+        dist_rows = c->dist_scratch.as<double>();
+    }
     {
         TimedLaunch t(c, "graph_emit", bytes, 0);
         HIP_TRY(c, launch_graph_emit(c->stream, g, cap, stage, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
-                                     const_cast<int64_t*>(row_ptr), col, dist, disp, rbf, rs, &sc->graph_flag));
+                                     const_cast<int64_t*>(row_ptr), col, dist_rows, disp, rbf, rs, &sc->graph_flag));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->emit_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     c->emit_pending = true;
@@ -780,6 +787,51 @@ int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, do
         }
     }
     return st;
+}
+
+int dgn_debug_betti_clouds(dgn_ctx* c, const dgn_batch* h, double rc, int64_t first, int64_t count, int32_t max_points,
+                           float* lower, int32_t* npoints, int64_t* keys) {
+    if (!c || !h || !lower || !npoints || first < 0 || count < 0 || first + count > h->num_atoms || max_points < 1)
+        return fail(c, DGN_ERR_ARG, "dgn_debug_betti_clouds: bad args");
+    if (count == 0) return DGN_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    dgn_batch d;
+    int st = stage_batch(c, h, &d);
+    if (st) return st;
+    int64_t E = 0;
+    st = graph_count_impl(c, &d, rc, UINT64_MAX, 1e-10, &E, true);
+    if (st) return st;
+    if ((int64_t)c->bw.max_candidates + 1 > max_points || max_points > betti_max_points())
+        return fail(c, DGN_ERR_CAPACITY, "dgn_debug_betti_clouds: a complex has " +
+                                             std::to_string(c->bw.max_candidates + 1) + " points");
+    const int64_t tri = (int64_t)max_points * (max_points - 1) / 2;
+    const int64_t tri_stride = std::max<int64_t>(4, (tri + 3) / 4 * 4);
+    DevBuf dl, dn, dk;
+    hipError_t e;
+    if ((e = dl.ensure(4 * (size_t)(count * tri_stride))) || (e = dn.ensure(4 * (size_t)count)) ||
+        (e = dk.ensure(8 * (size_t)(count * max_points))))
+        return hip_fail(c, e, "dgn_debug_betti_clouds: allocation");
+    HIP_TRY(c, hipMemsetAsync(dl.p, 0, 4 * (size_t)(count * tri_stride), c->stream));
+    HIP_TRY(c, hipMemsetAsync(dk.p, 0, 8 * (size_t)(count * max_points), c->stream));
+    HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, sizeof(uint32_t), c->stream));
+    const GraphLaunch g = graph_launch(c->bw, &d, rc, 1e-10, UINT64_MAX, true);
+    HIP_TRY(c, launch_betti_dist_search(c->stream, g, first, count, max_points, tri_stride, c->bw.counts.as<int32_t>(),
+                                        dl.as<float>(), dn.as<int32_t>(), &sc->graph_flag, dk.as<uint64_t>(),
+                                        max_points));
+    HIP_TRY(c, hipMemcpyAsync(&c->host->s.graph_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->host->s.graph_flag)
+        return fail(c, DGN_ERR_INTERNAL, "dgn_debug_betti_clouds: search disagreed with the count pass");
+    std::vector<float> tmp((size_t)(count * tri_stride));
+    if ((e = hipMemcpy(tmp.data(), dl.p, 4 * tmp.size(), hipMemcpyDeviceToHost)) ||
+        (e = hipMemcpy(npoints, dn.p, 4 * (size_t)count, hipMemcpyDeviceToHost)) ||
+        (keys && (e = hipMemcpy(keys, dk.p, 8 * (size_t)(count * max_points), hipMemcpyDeviceToHost))))
+        return hip_fail(c, e, "dgn_debug_betti_clouds: copy back");
+    for (int64_t i = 0; i < count; ++i) std::memcpy(lower + i * tri, tmp.data() + i * tri_stride, 4 * (size_t)tri);
+    return DGN_OK;
 }
 
 static int host_persistence_common(dgn_ctx* c, const double* clouds, const float* lower, const int32_t* npoints,

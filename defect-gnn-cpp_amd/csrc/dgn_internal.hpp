@@ -132,9 +132,11 @@ hipError_t launch_betti_dist(hipStream_t s, const BettiLaunch& b, const DistLaun
 // distance pass with its own neighbour search (graph_kernels.hip): complex c = atom first + c,
 // cloud = centre + every neighbour within rc (betti_features.cpp:67-73, NeighborList(rc, inf));
 // writes the packed f32 lower triangle and npoints; counts = the count pass's per-atom m.
+// keys_out (diagnostics, may be null): [count][key_stride] packed (j, image) of cloud rows 1..m
 hipError_t launch_betti_dist_search(hipStream_t s, const GraphLaunch& g, int64_t first, int64_t count,
                                     int max_points, int64_t tri_stride, const int32_t* counts, float* lower,
-                                    int32_t* npoints, uint32_t* error_flag);
+                                    int32_t* npoints, uint32_t* error_flag, uint64_t* keys_out = nullptr,
+                                    int key_stride = 0);
 int betti_max_points();      // largest local complex (centre + neighbours) the kernel accepts
 int64_t betti_scratch_bytes_per_wave();
 // fresh per-wave scratch: every min-cofacet byte "no cofacet" (0xFF), never a clearing mark

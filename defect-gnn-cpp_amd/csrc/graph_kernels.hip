@@ -294,9 +294,9 @@ __device__ __forceinline__ StructMeta load_meta_uniform(const StructMeta* p) {
 
 template <class PerAtom>
 __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const StageView st, int64_t a_begin,
-                                                int64_t a_end, PerAtom&& per_atom) {
+                                                int64_t a_end, int64_t tile, PerAtom&& per_atom) {
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    const int64_t g0 = a_begin + (int64_t)blockIdx.x * kQA;
+    const int64_t g0 = a_begin + tile * kQA;
     const int64_t g1 = g0 + kQA < a_end ? g0 + kQA : a_end;
     if (g0 >= g1) return;
     const int32_t b_first = uni_i32(g.atom_struct[g0]);
@@ -408,34 +408,71 @@ __device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq,
     return (dx * dx + dy * dy) + dz * dz;
 }
 
-// Count pass on a staged one-image structure: lane j decides atom j from the approximate distance;
-// only candidates within the band around rc (a handful per million) take the exact reference
-// test. The self image (j == li, n = 0) is the only image of the query atom within rc. Returns
-// m; mask[t] = the hit ballot of atom tile t (a bit per atom).
+// Count pass on a staged one-image structure: each lane decides atoms base + lane and base + 64 +
+// lane from an approximate nearest-image distance computed for both at once in packed f32
+// (v_pk_fma_f32); only candidates within `band32` of rc^2 (a few per thousand queries) take the
+// exact reference test in f64. The self image (j == li, n = 0) is the only image of the query
+// atom within rc. Returns m; mask[t] = the hit ballot of atom tile t (a bit per atom).
+//   band32 bounds |approx - exact| for candidates with either value below rc^2 + band32: the
+//   fixed-point quantisation (M.band), f32 displacement error eps <= 5 * 2^-24 * 0.5 * sum|L| per
+//   axis (conversion of the 32-bit fraction, the rounded f32 lattice, product, two sums),
+//   2 sqrt(3) R eps + 3 eps^2 on the square (R = rc + 1e-3 bounds |d|), 3 * 2^-24 R^2 for the
+//   f32 square and sums, 2^-20 rc^2 for rounding the thresholds; the sum is doubled.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int count_staged_one(const StructMeta& M, const StageView st, const double q[3], int li,
                                                 double rc2, DGN_LDS uint64_t* mask_words) {
     const int lane = lane_id();
     const int natoms = M.natoms;
     const u32x4 fq = st.fx[li];
-    const double lo = rc2 - M.band, hi = rc2 + M.band;
+    double lsum = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) lsum += fabs(M.L[k]);
+    const double eps = 5.0 * 0x1p-24 * 0.5 * lsum, R = sqrt(rc2) + 1e-3;
+    const double band32 =
+        2.0 * (M.band + 2.0 * 1.7320508075688772 * R * eps + 3.0 * eps * eps + 3.0 * 0x1p-24 * R * R + 0x1p-20 * rc2);
+    const float lo32 = (float)(rc2 - band32), hi32 = (float)(rc2 + band32);
+    float Lf[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Lf[k] = (float)(M.L[k] * 0x1p-32);
     int m = 0;
-    for (int base = 0, t = 0; base < natoms; base += kWave, ++t) {
-        const int j = base + lane;
-        bool hit = false;
-        if (j < natoms && j != li) {
-            const u32x4 fj = st.fx[j];
-            const double d2a = approx_d2(M, fq, fj);
-            hit = d2a < lo;
-            if (d2a >= lo && d2a <= hi) {  // borderline: the exact reference arithmetic decides
-                int n[3];
-                bool inr;
-                const double d2 = exact_one(st, fq, fj, j, q, n, inr);
-                hit = inr && d2 < rc2;
-            }
+    for (int base = 0, t = 0; base < natoms; base += 2 * kWave, t += 2) {
+        const int j0 = base + lane, j1 = base + kWave + lane;
+        const u32x4 a = st.fx[j0 < natoms ? j0 : natoms - 1];
+        const u32x4 c = st.fx[j1 < natoms ? j1 : natoms - 1];
+        const f32x2 u0 = {(float)(int)(a.x - fq.x), (float)(int)(c.x - fq.x)};
+        const f32x2 u1 = {(float)(int)(a.y - fq.y), (float)(int)(c.y - fq.y)};
+        const f32x2 u2 = {(float)(int)(a.z - fq.z), (float)(int)(c.z - fq.z)};
+        f32x2 dx, dy, dz;
+        if (M.diag) {
+            dx = u0 * Lf[0];
+            dy = u1 * Lf[4];
+            dz = u2 * Lf[8];
+        } else {
+            dx = __builtin_elementwise_fma(u2, (f32x2)Lf[6], __builtin_elementwise_fma(u1, (f32x2)Lf[3], u0 * Lf[0]));
+            dy = __builtin_elementwise_fma(u2, (f32x2)Lf[7], __builtin_elementwise_fma(u1, (f32x2)Lf[4], u0 * Lf[1]));
+            dz = __builtin_elementwise_fma(u2, (f32x2)Lf[8], __builtin_elementwise_fma(u1, (f32x2)Lf[5], u0 * Lf[2]));
         }
-        const uint64_t bal = ballot(hit);
-        if (mask_words && lane == 0) mask_words[t] = bal;
-        m += __popcll(bal);
+        const f32x2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
+        const bool ok0 = j0 < natoms && j0 != li, ok1 = j1 < natoms && j1 != li;
+        bool hit0 = ok0 && d2.x < lo32, hit1 = ok1 && d2.y < lo32;
+        if (ok0 && !hit0 && d2.x <= hi32) {  // borderline: the exact reference arithmetic decides
+            int n[3];
+            bool inr;
+            const double e2 = exact_one(st, fq, a, j0, q, n, inr);
+            hit0 = inr && e2 < rc2;
+        }
+        if (ok1 && !hit1 && d2.y <= hi32) {
+            int n[3];
+            bool inr;
+            const double e2 = exact_one(st, fq, c, j1, q, n, inr);
+            hit1 = inr && e2 < rc2;
+        }
+        const uint64_t bal0 = ballot(hit0), bal1 = ballot(hit1);
+        if (mask_words && lane == 0) {
+            mask_words[t] = bal0;
+            if (base + kWave < natoms) mask_words[t + 1] = bal1;
+        }
+        m += __popcll(bal0) + __popcll(bal1);
     }
     return m;
 }
@@ -512,7 +549,9 @@ __device__ __forceinline__ int collect_mask_hits(const DGN_LDS uint64_t* mask, i
     const int lane = lane_id();
     int m = 0;
     for (int t = 0; 64 * t < natoms; ++t) {
-        const uint64_t word = mask[t];  // broadcast read
+        const uint64_t wv = mask[t];  // broadcast read
+        const uint64_t word = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(wv >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wv);
         if ((word >> lane) & 1ull) hit[m + mask_prefix(word)] = (uint32_t)(64 * t + lane);
         m += __popcll(word);
     }
@@ -661,7 +700,10 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
 // size). No atomics. For staged one-image structures it also records each query's exact hits as
 // a bit per atom (mask[gi][kMaskWords]) so the emit and Betti passes skip the search.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
+#ifndef DGN_COUNT_WAVES
+#define DGN_COUNT_WAVES 4
+#endif
+__global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT_WAVES))) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
                                                                    int64_t* __restrict__ block_sums,
                                                                    uint64_t* __restrict__ block_aux,
                                                                    uint64_t* __restrict__ mask_out) {
@@ -678,7 +720,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_count_kernel(GraphLaunch g,
     int64_t my_sum = 0;
     uint32_t my_max = 0, my_nat = 0;
     uint64_t my_sq = 0;
-    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
+    for_block_atoms(g, st, 0, g.num_atoms, blockIdx.x, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
@@ -793,26 +835,37 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
 // Ranking of one atom's compacted hits by (distance, j, image), the canonical row order.
 // ------------------------------------------------------------------------------------------
 // m <= 64: lane s ranks entry s by counting strictly smaller distances (broadcast LDS reads, one
-// f64 compare each); exact distance ties collide on a rank, which a claim byte detects, and only
-// then is the (j, image) tie-break counted.
+// f64 compare each; 8 entries per step with the next step's reads in flight; kd[m, round8(m)) must
+// hold +inf); exact distance ties collide on a rank, which a claim byte detects, and only then is
+// the (j, image) tie-break counted.
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int rank_small(const DGN_LDS double* kd, const DGN_LDS uint64_t* kj, int m,
                                           DGN_LDS uint8_t* claim) {
+    m = uni_i32(m);
     const int lane = lane_id();
     const bool act = lane < m;
     const double me = act ? kd[lane] : 0.0;
-    int r = 0, u = 0;
-    for (; u + 4 <= m; u += 4) {
-        const double a = kd[u], b = kd[u + 1], c = kd[u + 2], e = kd[u + 3];
-        r += (int)(a < me) + (int)(b < me) + (int)(c < me) + (int)(e < me);
+    const DGN_LDS f64x2* kv = reinterpret_cast<const DGN_LDS f64x2*>(kd);
+    const int m8 = (m + 7) >> 3;
+    int r = 0;
+    f64x2 c0 = kv[0], c1 = kv[1], c2 = kv[2], c3 = kv[3];
+    for (int s = 0; s < m8; ++s) {
+        const int nx = s + 1 < m8 ? 4 * (s + 1) : 4 * s;
+        const f64x2 n0 = kv[nx], n1 = kv[nx + 1], n2 = kv[nx + 2], n3 = kv[nx + 3];
+        r += ((int)(c0.x < me) + (int)(c0.y < me)) + ((int)(c1.x < me) + (int)(c1.y < me)) +
+             ((int)(c2.x < me) + (int)(c2.y < me)) + ((int)(c3.x < me) + (int)(c3.y < me));
+        c0 = n0;
+        c1 = n1;
+        c2 = n2;
+        c3 = n3;
     }
-    for (; u < m; ++u) r += (int)(kd[u] < me);
     if (act) claim[r] = (uint8_t)lane;
     wave_lds_sync();
     const bool lost = act && claim[r] != (uint8_t)lane;
     if (ballot(lost)) {
         const uint64_t mj = act ? kj[lane] : 0ull;
         int extra = 0;
-        for (u = 0; u < m; ++u) extra += (int)((kd[u] == me) & (kj[u] < mj));
+        for (int u = 0; u < m; ++u) extra += (int)((kd[u] == me) & (kj[u] < mj));
         r += extra;
     }
     return r;
@@ -918,28 +971,49 @@ __device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, c
 }
 
 // ------------------------------------------------------------------------------------------
-// Block RBF stream (STREAM emit): the block's edges are processed EP at a time per wave; lane =
+// Block RBF stream (STREAM emit): the block's edges (distances re-read from the just written
+// `dist` rows, L2-resident) are processed EP at a time per wave; lane =
 // (edge, segment of h bins). With t0 = k0 dr - d the segment start's offset from the centre,
 //   g_{k0+i} = norm exp(-0.5 (t0 + i dr)^2 / s^2) = G_i C_i,   G_i = g_{k0} B^i,
 //   B = exp(-t0 dr / s^2),   C_i = exp(-0.5 i^2 dr^2 / s^2)  (table),
-// so each value costs two f64 multiplies (G_{i+1} = G_i B, G_i C_i) after two exps per lane; the
-// running product carries i + 3 roundings (<= 1e-14 relative for i <= 100, far inside the f64
-// path's 1e-13 and the f32 path's 1e-6). Values go to a per-wave LDS buffer laid out like the
-// output (shifted to the output's 16-byte phase) and leave as non-temporal 16-byte stores.
+// G_i runs as an f64 product chain (<= 1e-14 relative for i <= 100). f64 output: G_i C_i in f64.
+// f32 output: per pair of bins, g = f32(G_i), (g, g f32(B)) x (C_i, C_{i+1}) as one packed f32
+// multiply, G_{i+2} = G_i B^2 in f64: at most 5 f32 roundings, < 3.5e-7 relative, inside the f32
+// path's 1e-6. Values go to a per-wave LDS buffer laid out like the output (shifted to the
+// output's 16-byte phase) and leave as non-temporal 16-byte stores.
 // ------------------------------------------------------------------------------------------
+#ifndef DGN_RBF_BUF_BYTES
+#define DGN_RBF_BUF_BYTES 4352  // per wave: 21 edges x 50 f32 bins
+#endif
 struct RbfStreamGeom {
     int ep, seg, h;  // edges per pass, lanes per edge, bins per lane
 };
 __host__ __device__ inline RbfStreamGeom rbf_stream_geom(int nb, int elem) {
-    constexpr int kBufBytes = 4096;  // per wave
-    int ep = kBufBytes / (nb * elem);
-    ep = ep < 1 ? 1 : (ep > kWave ? kWave : ep);
-    int sg = kWave / ep;
+    // fewest lanes per edge (most edges per exp pair) whose pass fits the buffer
+    int sg = 1;
+    while (sg < kWave && (kWave / sg) * nb * elem + 16 > DGN_RBF_BUF_BYTES) ++sg;
+    int ep = kWave / sg;
+    if (ep < 1) ep = 1;
     sg = sg > nb ? nb : sg;
     return {ep, sg, (nb + sg - 1) / sg};
 }
+__host__ __device__ inline int rbf_stream_buf_bytes(const RbfStreamGeom& gm, int nb, int elem) {
+    return ((gm.ep * nb + 16 / elem) * elem + 16 + 15) / 16 * 16;
+}
+// exp(x) for |x| < 700 (no range checks): x = n ln2 + r, |r| <= ln2 / 2, Taylor of degree DEG in
+// r (DEG 12: < 2e-16 truncation; DEG 8: < 6e-9), times 2^n
+template <int DEG>
+__device__ __forceinline__ double exp_bounded(double x) {
+    const double n = __builtin_rint(x * 1.4426950408889634);
+    double r = __builtin_fma(-n, 6.93147180369123816490e-01, x);
+    r = __builtin_fma(-n, 1.90821492927058770002e-10, r);
+    double p = 1.0;
+#pragma unroll
+    for (int k = DEG; k >= 1; --k) p = __builtin_fma(p, r * (1.0 / k), 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
 template <typename T>
-__device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, const DGN_LDS double* dl,
+__device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, const double* __restrict__ dl,
                                                 const DGN_LDS double* ctab, DGN_LDS T* buf, const RbfSpec& rs,
                                                 const RbfStreamGeom gm, int w) {
     constexpr int V = 16 / sizeof(T);
@@ -948,20 +1022,60 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
     const int le = lane / gm.seg, sgi = lane - le * gm.seg;
     const int k0 = sgi * gm.h;
     const int cnt0 = nb - k0 < gm.h ? nb - k0 : gm.h;
+    const DGN_LDS f32x2* ctf = reinterpret_cast<const DGN_LDS f32x2*>(ctab + gm.h + 1);  // f32 (C_i, C_i+1)
+    // the next pass's distance is loaded while this pass computes and streams
+    double dnext = (w * gm.ep + le < ne && le < gm.ep) ? dl[w * gm.ep + le] : 0.0;
     for (int e = w * gm.ep; e < ne; e += kW * gm.ep) {
         const int nedge = ne - e < gm.ep ? ne - e : gm.ep;
         T* o = out + (int64_t)e * nb;
         const int phase = (int)(((uintptr_t)o / sizeof(T)) & (V - 1));  // o - phase is 16-byte aligned
+        const double d = dnext;
+        {
+            const int en = e + kW * gm.ep + le;
+            dnext = (en < ne && le < gm.ep) ? dl[en] : 0.0;
+        }
         if (le < nedge && cnt0 > 0) {
-            const double d = dl[e + le];
             const double t0 = (double)k0 * rs.dr - d;
             const double s = rs.inv_sigma2;
-            double G = rs.norm * exp(-0.5 * (t0 * t0) * s);
-            const double B = exp(-(t0 * rs.dr) * s);
             DGN_LDS T* dst = buf + phase + le * nb + k0;
-            for (int i = 0; i < cnt0; ++i) {
-                dst[i] = (T)(G * ctab[i]);
-                G *= B;
+            if constexpr (sizeof(T) == 8) {
+                double G = rs.norm * exp_bounded<12>(-0.5 * (t0 * t0) * s);
+                const double B = exp_bounded<12>(-(t0 * rs.dr) * s);
+                for (int i = 0; i < cnt0; ++i) {
+                    dst[i] = G * ctab[i];
+                    G *= B;
+                }
+            } else {
+                double G = rs.norm * exp_bounded<8>(-0.5 * (t0 * t0) * s);
+                const double B = exp_bounded<8>(-(t0 * rs.dr) * s);
+                const double B2 = B * B;
+                const float bf = (float)B;
+                int i = 0;
+                auto pair = [&](int at, const f32x2 c) __attribute__((always_inline)) {
+                    const float g = (float)G;
+                    const f32x2 gg = {g, g * bf};
+                    const f32x2 v = gg * c;
+                    dst[at] = v.x;
+                    dst[at + 1] = v.y;
+                    G *= B2;
+                };
+                for (; i + 8 <= cnt0; i += 8) {  // the table reads of 4 pairs in flight together
+                    const f32x2 c0 = ctf[(i >> 1)], c1 = ctf[(i >> 1) + 1], c2 = ctf[(i >> 1) + 2],
+                                c3 = ctf[(i >> 1) + 3];
+                    pair(i, c0);
+                    pair(i + 2, c1);
+                    pair(i + 4, c2);
+                    pair(i + 6, c3);
+                }
+                for (; i + 2 <= cnt0; i += 2) {
+                    const float g = (float)G;
+                    const f32x2 gg = {g, g * bf};
+                    const f32x2 v = gg * ctf[i >> 1];
+                    dst[i] = v.x;
+                    dst[i + 1] = v.y;
+                    G *= B2;
+                }
+                if (i < cnt0) dst[i] = (float)G * ctf[i >> 1].x;
             }
         }
         wave_lds_sync();
@@ -973,7 +1087,11 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
             if (f >= phase && f + V <= total) {
                 typedef T vec_t __attribute__((ext_vector_type(V)));
                 const vec_t val = *reinterpret_cast<const DGN_LDS vec_t*>(buf + f);
+#ifdef DGN_RBF_PLAIN_STORE
+                *reinterpret_cast<vec_t*>(o - phase + f) = val;
+#else
                 __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(o - phase + f));
+#endif
             } else {
                 for (int u = 0; u < V; ++u)
                     if (f + u >= phase && f + u < total) (o - phase)[f + u] = buf[f + u];
@@ -984,21 +1102,22 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 3: fused emit. Per atom (one wave): search, compact the hits into LDS, rank, write the
-// kept rows (col, distance, displacement). STREAM (max_neighbors <= kStreamMaxK): the kept
-// distances of the block's edges are kept in LDS and, after the block's atoms are done, its whole
-// RBF region (contiguous in the CSR) is written as one flat stream by all 256 threads; otherwise
-// each wave writes its atom's RBF block.
+// Kernel 3: fused emit. Per atom (one wave): compact the hits (the count pass's mask, or a search)
+// into LDS, rank, write the kept rows (col, distance, displacement). STREAM (max_neighbors <=
+// kStreamMaxK): after the block's atoms, its whole RBF region (contiguous in the CSR) is written
+// by the 4 waves from the block's distance rows, through per-wave LDS buffers as 16-byte
+// non-temporal stores; otherwise each wave writes its atom's RBF rows (write_rbf_flat).
+// `dist` must be non-null when STREAM writes an RBF (the host passes a scratch row buffer).
 // ------------------------------------------------------------------------------------------
-// Dynamic LDS of the emit (bytes): region A (search phase: stage, hit lists, hit masks) is dead
-// once the block's atoms are placed and is reused as region B (the per-wave RBF buffers); then
-// the block's rows (distances, columns) and the RBF C table, which live to the end.
+// Dynamic LDS of the emit (bytes): region A (search phase: stage, hit lists, hit masks, sorted
+// distances) is dead once the block's atoms are placed and is reused as region B (the per-wave
+// RBF buffers); then the RBF C table.
 struct EmitLayout {
-    int stage, keyd, keyj, mask, sorted, rbf, dl, colb, ctab, total;
+    int stage, keyd, keyj, mask, sorted, rbf, ctab, total;
     RbfStreamGeom gm;
+    int wbytes;
 };
-__host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool stream, int K, int nb, int elem,
-                                                  int nwm) {
+__host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool stream, int nb, int elem, int nwm) {
     EmitLayout l{};
     int o = 0;
     auto take = [&](int bytes) {
@@ -1013,15 +1132,37 @@ __host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool s
     l.sorted = take(stream ? 0 : kW * (cap + 1) * 8);
     const int a_end = o;
     l.gm = rbf_stream_geom(nb > 0 ? nb : 1, elem > 0 ? elem : 4);
-    const int b_bytes = (stream && nb > 0) ? kW * ((l.gm.ep * nb + 16 / (elem > 0 ? elem : 4)) * (elem > 0 ? elem : 4) + 16) : 0;
+    l.wbytes = (stream && nb > 0) ? rbf_stream_buf_bytes(l.gm, nb, elem > 0 ? elem : 4) : 0;
     l.rbf = 0;
-    o = a_end > b_bytes ? a_end : (b_bytes + 15) / 16 * 16;
-    l.dl = take(stream ? (kQA * K + 1) * 8 : 0);
-    l.colb = take(stream ? kQA * K * 4 : 0);
-    l.ctab = take(stream ? (l.gm.h + 1) * 8 : 0);
+    o = a_end > kW * l.wbytes ? a_end : (kW * l.wbytes + 15) / 16 * 16;
+    l.ctab = take(stream ? (l.gm.h + 1) * 8 + (l.gm.h + 2) * 4 : 0);  // f64 C_i, then f32 C_i
     l.total = o;
     return l;
 }
+
+// diagnostics build (-DDGN_EMIT_PHASES, never bench/tests): per-wave s_memtime cycles of the emit's
+// phases summed into dgn_emit_phase[] (read by dgn_diag_emit_phases)
+#ifdef DGN_EMIT_PHASES
+__device__ unsigned long long dgn_emit_phase[8];
+#define EMIT_STAMP(k)                                  \
+    do {                                               \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        ph[k] += t_ - tprev;                           \
+        tprev = t_;                                    \
+    } while (0)
+#else
+#define EMIT_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
+
+// the tiles (kQA atoms) of one emit launch: row tiles [row0, row0 + nrow) and RBF tiles
+// [rbf0, rbf0 + nrbf) whose rows an earlier launch wrote; fused: each row block streams its own
+// RBF after its rows (one launch, nrbf = 0)
+struct EmitTiles {
+    int64_t row0, nrow, rbf0, nrbf;
+    int fused;
+};
 
 template <int CAP, bool STREAM>
 __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, int stage_cap, int nwm,
@@ -1030,7 +1171,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                                                                   int64_t* __restrict__ row_ptr,
                                                                   int32_t* __restrict__ col, double* __restrict__ dist,
                                                                   double* __restrict__ disp, void* __restrict__ rbf,
-                                                                  RbfSpec rs, uint32_t* __restrict__ error_flag) {
+                                                                  RbfSpec rs, uint32_t* __restrict__ error_flag,
+                                                                  EmitTiles tl) {
     extern __shared__ double dyn[];
     __shared__ double4 offt_s[125];
     __shared__ uint32_t ring[kW][kRing];
@@ -1038,27 +1180,65 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     __shared__ int64_t row_start[kQA + 1];
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
     const int elem = rs.dtype == 2 ? 8 : 4;
-    const EmitLayout ly = emit_layout(stage_cap, CAP, STREAM, STREAM ? K : 0, rs.dtype ? rs.nbins : 0, elem, nwm);
+    const EmitLayout ly = emit_layout(stage_cap, CAP, STREAM, rs.dtype ? rs.nbins : 0, elem, nwm);
     DGN_LDS uint8_t* base = reinterpret_cast<DGN_LDS uint8_t*>(lds(dyn));
     const StageView st = make_stage(reinterpret_cast<double*>(dyn) + ly.stage / 8, stage_cap, offt_s);
     DGN_LDS double* key_d = reinterpret_cast<DGN_LDS double*>(base + ly.keyd);
     DGN_LDS uint64_t* key_j = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.keyj);
     DGN_LDS uint64_t* mask_s = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.mask);
     DGN_LDS double* sorted_d = reinterpret_cast<DGN_LDS double*>(base + ly.sorted);
-    DGN_LDS double* dl = reinterpret_cast<DGN_LDS double*>(base + ly.dl);
-    DGN_LDS int32_t* colb = reinterpret_cast<DGN_LDS int32_t*>(base + ly.colb);
     DGN_LDS double* ctab = reinterpret_cast<DGN_LDS double*>(base + ly.ctab);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int lane = lane_id();
-    const int64_t g0 = (int64_t)blockIdx.x * kQA;
+    // this block's job: row tiles and RBF tiles alternate in the grid (every CU gets both)
+    const int64_t both = tl.nrow < tl.nrbf ? tl.nrow : tl.nrbf;
+    const int64_t x = blockIdx.x;
+    const bool is_rbf = x < 2 * both ? (x & 1) != 0 : tl.nrbf > tl.nrow;
+    const int64_t tile = (is_rbf ? tl.rbf0 : tl.row0) + (x < 2 * both ? x >> 1 : x - both);
+    const int64_t g0 = tile * kQA;
     const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
+#ifdef DGN_EMIT_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tprev = __builtin_amdgcn_s_memtime();
+#endif
+    // the RBF of this tile from its rows (row_ptr, dist), by the block's 4 waves; region A must be dead
+    auto rbf_tile = [&]() __attribute__((always_inline)) {
+        for (int i = threadIdx.x; i <= ly.gm.h + 1; i += kGraphBlock) {
+            const double xx = (double)i * rs.dr;
+            const double c = exp(-0.5 * (xx * xx) * rs.inv_sigma2);  // C_i
+            if (i <= ly.gm.h) ctab[i] = c;
+            reinterpret_cast<DGN_LDS float*>(ctab + ly.gm.h + 1)[i] = (float)c;
+        }
+        __syncthreads();
+        // the tile's own rows only: row_ptr[g0 + nq] belongs to the next tile, whose rows may be
+        // written by this same launch
+        const int64_t e0 = row_ptr[g0], e1 = row_ptr[g0 + nq - 1] + counts[g0 + nq - 1];
+        const int ne = (int)(e1 - e0);
+        if (rs.dtype == 1)
+            rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dist + e0, ctab,
+                            reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
+        else
+            rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dist + e0, ctab,
+                            reinterpret_cast<DGN_LDS double*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
+        EMIT_STAMP(4);
+    };
+    if constexpr (STREAM) {
+        if (is_rbf) {
+            rbf_tile();
+#ifdef DGN_EMIT_PHASES
+            if (lane == 0 && (blockIdx.x & 63) == 1)
+                for (int k = 0; k < 8; ++k) atomicAdd(&dgn_emit_phase[k], (unsigned long long)ph[k]);
+#endif
+            return;
+        }
+    }
 
     // local scan of this block's counts -> row starts (and row_ptr); kQA == one wave
     if (w == 0) {
         const int64_t gi = g0 + lane;
         const int64_t c = gi < g.num_atoms ? counts[gi] : 0;
         const int64_t inc = wave_inclusive_sum(c);
-        const int64_t start = block_offsets[blockIdx.x] + inc - c;
+        const int64_t start = block_offsets[tile] + inc - c;
         row_start[lane] = start;
         if (lane == kWave - 1) row_start[kQA] = start + c;
         if (gi < g.num_atoms) {
@@ -1072,18 +1252,14 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             const int a_ = x / nwm, wd = x - a_ * nwm;
             mask_s[x] = g.mask[(g0 + a_) * kMaskWords + wd];
         }
-    // C_i = exp(-0.5 i^2 dr^2 / s^2) of the RBF stream
-    if (STREAM && rs.dtype != 0)
-        for (int i = threadIdx.x; i <= ly.gm.h; i += kGraphBlock) {
-            const double x = (double)i * rs.dr;
-            ctab[i] = exp(-0.5 * (x * x) * rs.inv_sigma2);
-        }
     __syncthreads();
-    const int64_t e0 = row_start[0];
+    EMIT_STAMP(0);
     DGN_LDS double* kd = key_d + w * CAP;
     DGN_LDS uint64_t* kj = key_j + w * CAP;
-    for_block_atoms(g, st, 0, g.num_atoms, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
+    DGN_LDS double* sd = sorted_d + w * (CAP + 1);
+    for_block_atoms(g, st, 0, g.num_atoms, tile, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
                                                __attribute__((always_inline)) {
+        EMIT_STAMP(1);
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
@@ -1132,6 +1308,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 }
                 m += __popcll(bal);
             });
+        EMIT_STAMP(2);
         const int64_t rs0 = row_start[t];
         const int kept = (int)(row_start[t + 1] - rs0);
         if (m > CAP || kept != (m < K ? m : K)) {
@@ -1151,14 +1328,9 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             const int64_t e = rs0 + rank;
             int j, na, nb, nc;
             unpack_jimg(key, j, na, nb, nc);
-            if constexpr (STREAM) {
-                dl[e - e0] = d;
-                colb[e - e0] = j;
-            } else {
-                sorted_d[w * (CAP + 1) + rank] = d;
-                col[e] = j;
-                if (dist) dist[e] = d;
-            }
+            if constexpr (!STREAM) sd[rank] = d;
+            col[e] = j;
+            if (dist) dist[e] = d;
             if (disp) {
                 double pj[3];
                 P.get(j, pj);
@@ -1169,6 +1341,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             }
         };
         if (m <= kWave) {
+            if (lane >= m && lane < ((m + 7) & ~7)) kd[lane] = __builtin_inf();  // rank_small reads groups of 8
+            wave_lds_sync();
 #ifdef DGN_EMIT_NORANK
             const int r = lane;  // A/B diagnostics only: rows in search order
 #else
@@ -1179,40 +1353,29 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             rank_large(kd, kj, m, put);
         }
         wave_lds_sync();
+        EMIT_STAMP(3);
         if constexpr (!STREAM) {
-            // 3. this atom's RBF block: kept x nbins contiguous values from rs0 * nbins
+            // 3. this atom's RBF rows: kept x nbins contiguous values from rs0 * nbins
             if (rs.dtype != 0 && rbf) {
                 const int total = kept * rs.nbins;
                 if (rs.dtype == 1)
-                    write_rbf_flat(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, sorted_d + w * (CAP + 1), rs,
-                                   lane, kWave);
+                    write_rbf_flat(reinterpret_cast<float*>(rbf) + rs0 * rs.nbins, total, sd, rs, lane, kWave);
                 else
-                    write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sorted_d + w * (CAP + 1), rs,
-                                   lane, kWave);
+                    write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sd, rs, lane, kWave);
             }
             wave_lds_sync();
         }
     });
     if constexpr (STREAM) {
-        __syncthreads();  // region A (stage, hit lists) is dead from here: region B reuses it
-        // the block's rows [e0, e1): columns and distances, coalesced
-        const int ne = (int)(row_start[kQA] - e0);
-        for (int i = threadIdx.x; i < ne; i += kGraphBlock) {
-            col[e0 + i] = colb[i];
-            if (dist) dist[e0 + i] = dl[i];
+        if (tl.fused) {
+            __syncthreads();  // the block's rows are written (visible to its waves); region A is dead
+            rbf_tile();
         }
-        if (rs.dtype == 0 || !rbf) return;
-#ifdef DGN_EMIT_NORBF
-        return;  // A/B diagnostics only
-#endif
-        const int wbytes = ((ly.gm.ep * rs.nbins + 16 / elem) * elem + 16);
-        if (rs.dtype == 1)
-            rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
-                            reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * wbytes), rs, ly.gm, w);
-        else
-            rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
-                            reinterpret_cast<DGN_LDS double*>(base + ly.rbf + w * wbytes), rs, ly.gm, w);
     }
+#ifdef DGN_EMIT_PHASES
+    if (lane == 0 && (blockIdx.x & 63) == 0)  // sampled: 1 block in 64 (atomics on 8 words serialise)
+        for (int k = 0; k < 8; ++k) atomicAdd(&dgn_emit_phase[k], (unsigned long long)ph[k]);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1229,7 +1392,9 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
                                                                          const int32_t* __restrict__ counts,
                                                                          float* __restrict__ lower,
                                                                          int32_t* __restrict__ npoints,
-                                                                         uint32_t* __restrict__ error_flag) {
+                                                                         uint32_t* __restrict__ error_flag,
+                                                                         uint64_t* __restrict__ keys_out,
+                                                                         int key_stride) {
     __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
     DGN_SEARCH_SMEM
     __shared__ uint64_t key_j[kW][CAP];
@@ -1245,7 +1410,7 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
             mask_s[x / kMaskWords][x % kMaskWords] = g.mask[g0 * kMaskWords + x];
         __syncthreads();
     }
-    for_block_atoms(g, st, first, first + count, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {
+    for_block_atoms(g, st, first, first + count, blockIdx.x, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         const int64_t c = gi - first;
         double q[3];
@@ -1290,6 +1455,8 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
             return;
         }
         wave_lds_sync();
+        if (keys_out)  // diagnostics (dgn_debug_betti_clouds): cloud row p >= 1 is (j, image) key p - 1
+            for (int p = lane; p < m && p < key_stride; p += kWave) keys_out[c * key_stride + p] = key_j[w][p];
         // cloud row p: p = 0 the centre, else centre + ((p_j + offset) - centre)
         auto point = [&](int p, double x[3]) __attribute__((always_inline)) {
             if (p == 0) {
@@ -1321,15 +1488,15 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
 
 hipError_t launch_betti_dist_search(hipStream_t s, const GraphLaunch& g, int64_t first, int64_t count, int max_points,
                                     int64_t tri_stride, const int32_t* counts, float* lower, int32_t* npoints,
-                                    uint32_t* error_flag) {
+                                    uint32_t* error_flag, uint64_t* keys_out, int key_stride) {
     if (count <= 0) return hipSuccess;
     const int64_t nb = graph_blocks(count);
     if (max_points <= kWave)
         hipLaunchKernelGGL(betti_dist_search_kernel<kWave>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, first,
-                           count, tri_stride, counts, lower, npoints, error_flag);
+                           count, tri_stride, counts, lower, npoints, error_flag, keys_out, key_stride);
     else
         hipLaunchKernelGGL(betti_dist_search_kernel<kWideMaxPoints>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g,
-                           first, count, tri_stride, counts, lower, npoints, error_flag);
+                           first, count, tri_stride, counts, lower, npoints, error_flag, keys_out, key_stride);
     return hipGetLastError();
 }
 
@@ -1406,12 +1573,56 @@ template <int CAP, bool STREAM>
 static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const int32_t* counts,
                           const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
                           void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
-    const int64_t nb = graph_blocks(g.num_atoms);
+    const int64_t nt = graph_blocks(g.num_atoms);
     const int nwm = (stage + 63) / 64;
-    const int K = STREAM ? (int)g.kmax : 0;
-    const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
-    hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)nb), dim3(kGraphBlock), (size_t)ly.total, s, g,
-                       stage, nwm, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
+    const EmitLayout ly = emit_layout(stage, CAP, STREAM, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
+    auto go = [&](EmitTiles tl) {
+        const int64_t blocks = tl.nrow + tl.nrbf;
+        if (blocks > 0)
+            hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)blocks), dim3(kGraphBlock),
+                               (size_t)ly.total, s, g, stage, nwm, counts, block_offsets, row_ptr, col, dist, disp, rbf,
+                               rs, error_flag, tl);
+    };
+#ifdef DGN_EMIT_NORBF
+    go({0, nt, 0, 0, 0});  // A/B diagnostics only: rows without the RBF
+    return;
+#endif
+    if (!STREAM || rs.dtype == 0 || !rbf) {
+        go({0, nt, 0, 0, 0});
+        return;
+    }
+    static const bool pipeline = [] {
+        const char* e = getenv("DGN_EMIT_PIPELINE");
+        return e && e[0] == '1';
+    }();
+    if (!pipeline) {
+        go({0, nt, 0, 0, 1});  // each block: rows, then its RBF
+        return;
+    }
+    // Pipeline (DGN_EMIT_PIPELINE=1, measured slower on MI355X: RBF blocks alone stream at ~4 TB/s
+    // and take slots from the row blocks): launch i writes the rows of chunk i and the RBF of
+    // chunk i - 1 (its rows complete at the launch boundary). Chunks: 1/16 at both ends (the
+    // unpaired head and tail), 2/16 in between.
+    constexpr int kParts = 16;
+    int64_t bnd[10];
+    int nb = 0;
+    bnd[nb++] = 0;
+    if (nt >= 4 * kParts) {
+        for (int p = 1; p < kParts; p += 2) bnd[nb++] = nt * p / kParts;
+    }
+    bnd[nb++] = nt;
+    for (int i = 0; i < nb; ++i) {
+        EmitTiles tl{0, 0, 0, 0, 0};
+        if (i + 1 < nb) {
+            tl.row0 = bnd[i];
+            tl.nrow = bnd[i + 1] - bnd[i];
+        }
+        if (i > 0) {
+            tl.rbf0 = bnd[i - 1];
+            tl.nrbf = bnd[i] - bnd[i - 1];
+        }
+        go(tl);
+    }
 }
 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
@@ -1440,3 +1651,16 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
 }
 
 }  // namespace dgn
+
+#ifdef DGN_EMIT_PHASES
+// diagnostics build only: read (and optionally clear) the emit phase cycles
+extern "C" int dgn_diag_emit_phases(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dgn::dgn_emit_phase), 8 * sizeof(unsigned long long)) != hipSuccess)
+        return -1;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(dgn::dgn_emit_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

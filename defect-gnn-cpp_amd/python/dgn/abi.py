@@ -21,7 +21,7 @@ EXPORTS = [
     "dgn_ctx_last_error", "dgn_ctx_enable_timing", "dgn_ctx_kernel_times", "dgn_ctx_reset_timing",
     "dgn_graph_params_default", "dgn_rbf_bins", "dgn_dev_graph_count", "dgn_dev_graph_emit", "dgn_host_graph",
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
-    "dgn_host_persistence_lower", "dgn_host_rbf",
+    "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch",
 ]
 
@@ -73,6 +73,14 @@ def lib():
         return _lib
     if not os.path.exists(lib_path):
         raise FileNotFoundError(f"{lib_path} missing: run `make` (or __graft_entry__.build()) first")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 (SONAMEs
+    # libamdhip64.so.7 / libhsa-runtime64.so.1), which libdgn's DT_NEEDED entries bind to when torch is
+    # loaded first; loaded the other way round the process would hold two runtimes and torch would
+    # find no device. So torch, when installed, is imported before libdgn.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(lib_path)
     vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     L.dgn_status_string.restype = C.c_char_p
@@ -100,6 +108,8 @@ def lib():
     L.dgn_host_persistence.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
     L.dgn_host_persistence_lower.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
     L.dgn_host_rbf.argtypes = [vp, vp, i64, dbl, dbl, i32, i32, vp]
+    if hasattr(L, "dgn_debug_betti_clouds"):  # absent from older A/B builds
+        L.dgn_debug_betti_clouds.argtypes = [vp, vp, dbl, i64, i64, i32, vp, vp, vp]
     L.dgn_synth_atoms_per_structure.restype = i64
     L.dgn_synth_atoms_per_structure.argtypes = [C.c_int, C.c_int]
     L.dgn_synth_batch.argtypes = [C.c_int, C.c_int, i64, i64, vp, vp, vp, vp]
@@ -246,6 +256,18 @@ class Context:
         self._check(lib().dgn_host_persistence_lower(self.h, _ptr(lower), _ptr(npoints), Cn, max_points, threshold,
                                                      _ptr(pairs), cap, _ptr(counts)), "dgn_host_persistence_lower")
         return pairs, counts
+
+    def debug_betti_clouds(self, batch: dict, r_cutoff: float, atom_first: int, count: int, max_points: int):
+        """Diagnostics: the Betti pass's local complexes of atoms [atom_first, atom_first + count):
+        (lower [count][C(max_points, 2)] f32 in the kernel's row order, npoints [count],
+        keys [count][max_points] int64 packed (j, image) of cloud rows 1..npoints-1)."""
+        b = make_batch(batch)
+        lower = np.zeros((count, max_points * (max_points - 1) // 2), np.float32)
+        npoints = np.zeros(count, np.int32)
+        keys = np.zeros((count, max_points), np.int64)
+        self._check(lib().dgn_debug_betti_clouds(self.h, C.byref(b), r_cutoff, atom_first, count, max_points,
+                                                 _ptr(lower), _ptr(npoints), _ptr(keys)), "dgn_debug_betti_clouds")
+        return lower, npoints, keys
 
     def host_rbf(self, distances, rbf_cutoff=10.0, rbf_dr=0.1, dtype=DGN_F64, layout=0):
         d = np.ascontiguousarray(distances, dtype=np.float64)

@@ -166,6 +166,16 @@ int dgn_host_persistence_lower(dgn_ctx* ctx, const float* lower, const int32_t* 
                                int32_t max_points, double threshold, float* pairs, int32_t cap,
                                int32_t* counts);
 
+/* Diagnostics (parity tests): the local complexes of atoms [atom_first, atom_first + count) of a
+ * host batch as the Betti pass's distance kernel builds them (NeighborList(rc, SIZE_MAX) search +
+ * MFMA Gram distances, betti_features.cpp:67-73 / ripser_wrapper.cpp:20-24). lower: [count]
+ * [max_points*(max_points-1)/2] f32 strict lower triangles in the kernel's cloud row order;
+ * npoints[count]; keys (optional): [count][max_points] int64, row p >= 1 of the cloud is neighbour
+ * key[p-1] = (j << 24) | (na+128) << 16 | (nb+128) << 8 | (nc+128) (atom j, lattice image
+ * (na, nb, nc)), row 0 the centre. DGN_ERR_CAPACITY if a complex exceeds max_points. */
+int dgn_debug_betti_clouds(dgn_ctx* ctx, const dgn_batch* host_batch, double r_cutoff, int64_t atom_first,
+                           int64_t count, int32_t max_points, float* lower, int32_t* npoints, int64_t* keys);
+
 /* ---- synthetic batches (bench/test inputs) -----------------------
  * kind 0 = simple cubic m^3 (s = 2.32 A), kind 1 = FCC m^3 cells (a = 3.684 A). Host arrays:
  * lattice [B][9], positions [B*n][3], species [B*n], atom_offset [B+1]. */

@@ -149,3 +149,61 @@ def test_betti_batch_with_dense_outlier(ctx):
         assert np.array_equal(c[sl], co), s
         np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
     assert sizes[1] > 48 and max(sizes[0], sizes[2]) <= 48, sizes
+
+
+def _kernel_vs_reference_triangles(lower, npts, keys, lat, pos, a, rc):
+    """Map the Betti distance kernel's cloud rows to the reference's (centre, then the
+    NeighborList(rc, inf) rows in canonical order, betti_features.cpp:67-73) through the (j, image)
+    keys, and return (kernel triangle, reference triangle re-indexed into the kernel's order)."""
+    nl = O.neighbor_list(lat, pos, rc, None)
+    r0, r1 = nl["row_ptr"][a], nl["row_ptr"][a + 1]
+    n = int(npts)
+    assert n == r1 - r0 + 1
+    cloud = np.vstack([pos[a], pos[a] + nl["disp"][r0:r1]])
+    ref_low = O.local_distances(cloud)
+    row_of = {(int(nl["col"][e]), *map(int, nl["image"][e])): e - r0 + 1 for e in range(r0, r1)}
+    perm = [0]
+    for p in range(n - 1):
+        k = int(keys[p])
+        j, na, nb, nc = k >> 24, ((k >> 16) & 255) - 128, ((k >> 8) & 255) - 128, (k & 255) - 128
+        perm.append(row_of[(j, na, nb, nc)])
+    assert sorted(perm) == list(range(n))
+    tri = lambda i, j: i * (i - 1) // 2 + j  # noqa: E731  (i > j)
+    mapped = np.empty(n * (n - 1) // 2, np.float32)
+    for i in range(1, n):
+        for j in range(i):
+            pi, pj = perm[i], perm[j]
+            mapped[tri(i, j)] = ref_low[tri(max(pi, pj), min(pi, pj))]
+    return lower[:n * (n - 1) // 2], mapped, cloud, ref_low
+
+
+@pytest.mark.parametrize("s", [0, 3, 7])
+def test_betti_dist_triangles_sc64_fixture(ctx, s):
+    """The Betti pass's own neighbour search + MFMA Gram distances: every entry of the f32 lower
+    triangle bit-identical to the reference arithmetic (sc64_rc5.npz lower0 / lower37, i.e.
+    ripser_wrapper.cpp:20-24 over betti_features.cpp:67-73's cloud)."""
+    fx = np.load(os.path.join(GOLDEN, "sc64_rc5.npz"))
+    batch = dgn.synth_batch("sc", 4, 8)
+    n = 64
+    one = {"lattice": batch["lattice"][s:s + 1].copy(), "positions": batch["positions"][s * n:(s + 1) * n].copy(),
+           "species": batch["species"][s * n:(s + 1) * n].copy(), "atom_offset": np.array([0, n], np.int64)}
+    for a in (0, 37):
+        lower, npts, keys = ctx.debug_betti_clouds(one, 5.0, a, 1, 64)
+        got, mapped, cloud, ref_low = _kernel_vs_reference_triangles(lower[0], npts[0], keys[0], one["lattice"][0],
+                                                                     one["positions"], a, 5.0)
+        assert np.array_equal(cloud, fx[f"{s}/cloud{a}"])
+        assert np.array_equal(ref_low, fx[f"{s}/lower{a}"])
+        assert np.array_equal(got.view(np.uint32), mapped.view(np.uint32)), (s, a)
+
+
+def test_betti_dist_triangles_fcc256(ctx):
+    """Same on FCC-256 complexes (43 points) against oracle_local_distances."""
+    batch = dgn.synth_batch("fcc", 4, 2)
+    n = 256
+    atoms = [0, 1, 100, 255, 256, 300, 511]
+    lower, npts, keys = ctx.debug_betti_clouds(batch, 5.0, 0, 2 * n, 64)
+    for gi in atoms:
+        s, a = divmod(gi, n)
+        got, mapped, _, _ = _kernel_vs_reference_triangles(lower[gi], npts[gi], keys[gi], batch["lattice"][s],
+                                                           batch["positions"][s * n:(s + 1) * n], a, 5.0)
+        assert np.array_equal(got.view(np.uint32), mapped.view(np.uint32)), gi
