@@ -7,7 +7,7 @@ BUILD    := $(PKG)/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I$(CSRC) -Iinclude
 LIB      := $(PKG)/lib/libdgn.so
 
-KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/dgn_api.o
+KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o
 
 all: $(LIB) facade oracle
 
@@ -60,12 +60,27 @@ $(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 $(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(DBUILD)
 	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -x hip -c $< -o $@
-$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/dgn_api.o
+$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/node_kernels.o $(DBUILD)/dgn_api.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 clean:
-	rm -rf $(BUILD) $(LIB) $(PKG)/build_diag* $(PKG)/lib/libdgn_diag*.so $(FACADE) $(FBIN)
+	rm -rf $(BUILD) $(SAN) $(LIB) $(PKG)/build_diag* $(PKG)/lib/libdgn_diag*.so $(FACADE) $(FBIN)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean diag facade
+
+# Host-code sanitizer run (ASan + UBSan) over the CPU oracle and the facade's host-only code
+# (parser, Structure, PCA): builds build_san/san_check and runs it on the POSCAR fixtures.
+SAN      := $(PKG)/build_san
+SANFLAGS := -O1 -g -std=c++17 -fno-omit-frame-pointer -ffp-contract=off -fsanitize=address,undefined \
+            -fno-sanitize-recover=undefined -Iinclude -I$(FDIR)/include -Ioracle
+sanitize: $(SAN)/san_check
+	mkdir -p $(SAN)/tmp
+	ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $(SAN)/san_check tests/golden/poscar $(SAN)/tmp
+$(SAN)/san_check: $(FDIR)/tools/san_check.cpp oracle/oracle.cpp oracle/oracle.h $(FDIR)/src/vasp_parser.cpp \
+                  $(FDIR)/src/structure.cpp $(FDIR)/src/pca.cpp $(FHDRS)
+	@mkdir -p $(SAN)
+	$(CXX) $(SANFLAGS) -o $@ $(FDIR)/tools/san_check.cpp oracle/oracle.cpp $(FDIR)/src/vasp_parser.cpp \
+	    $(FDIR)/src/structure.cpp $(FDIR)/src/pca.cpp
+.PHONY: sanitize

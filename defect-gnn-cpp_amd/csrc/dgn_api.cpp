@@ -763,6 +763,32 @@ int dgn_dev_betti(dgn_ctx* c, const dgn_batch* b, const dgn_betti_params* p, dou
     return betti_impl(c, b, p->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0);
 }
 
+int dgn_dev_node_features(dgn_ctx* c, const dgn_batch* b, const double* embed, int32_t num_keys, int32_t D,
+                          const double* betti, const double* pca_mean, const double* pca_components, int32_t k,
+                          double* out) {
+    if (!c || !b || b->num_atoms < 0 || (b->num_atoms > 0 && (!b->species || !out)) || !embed || num_keys <= 0 ||
+        D < 0 || k < 0 || k > 35 || (k > 0 && (!betti || !pca_mean || !pca_components)))
+        return fail(c, DGN_ERR_ARG, "dgn_dev_node_features: bad args");
+    if (b->num_atoms == 0) return DGN_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (int st = take_emit_flag(c)) return st;
+    HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
+    Scalars* sc = c->scalars.as<Scalars>();
+    HIP_TRY(c, hipMemsetAsync(&sc->error_flag, 0, sizeof(uint32_t), c->stream));
+    const double A = (double)b->num_atoms;
+    {
+        TimedLaunch t(c, "node_features", A * (4 + (k ? 35 * 8 : 0) + 8.0 * (D + k)), A * 2.0 * 35 * k);
+        HIP_TRY(c, launch_node_features(c->stream, b->species, b->num_atoms, embed, num_keys, D, k ? betti : nullptr,
+                                        pca_mean, pca_components, k, out, &sc->error_flag));
+    }
+    HIP_TRY(c, hipMemcpyAsync(&c->host->s.error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->host->s.error_flag)
+        return fail(c, DGN_ERR_ARG, "dgn_dev_node_features: a species key has no embedding row (atom_embeddings.at)");
+    return DGN_OK;
+}
+
 int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, double* features, int32_t* counts) {
     if (!c || !p || !features || !h || !h->species) return fail(c, DGN_ERR_ARG, "dgn_host_betti: bad args");
     HIP_TRY(c, hipSetDevice(c->device));

@@ -156,4 +156,11 @@ struct BettiFork {
 hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
                         int wide_waves, const BettiFork* fork = nullptr);
 
+// ---- node features (node_kernels.hip) ----
+// out[A][D + k]: embed[species[i]] (D f64) then (betti[i] - mean) * comp (k f64; comp row-major
+// 35 x k); error_flag bit 0: a species key outside [0, nkeys)
+hipError_t launch_node_features(hipStream_t s, const int32_t* species, int64_t A, const double* embed, int32_t nkeys,
+                                int32_t D, const double* betti, const double* mean, const double* comp, int32_t k,
+                                double* out, uint32_t* error_flag);
+
 }  // namespace dgn

@@ -249,10 +249,11 @@ struct StageView {
 };
 // stage bytes per atom: 3 doubles + one uint4
 constexpr int kStageBytesPerAtom = 3 * 8 + 16;
+// offt == nullptr: no offset table (exact_one computes each image offset)
 __device__ __forceinline__ StageView make_stage(double* base_, int cap, double4* offt) {
     DGN_LDS double* base = lds(base_);
     return {base, base + cap, base + 2 * cap, reinterpret_cast<DGN_LDS u32x4*>(base + 3 * cap),
-            reinterpret_cast<DGN_LDS f64x4*>(lds(offt)), cap};
+            offt ? reinterpret_cast<DGN_LDS f64x4*>(lds(offt)) : nullptr, cap};
 }
 __device__ __forceinline__ uint32_t pack_floors(const int s[3]) {
     return (uint32_t)(s[0] + 512) | ((uint32_t)(s[1] + 512) << 10) | ((uint32_t)(s[2] + 512) << 20);
@@ -323,7 +324,7 @@ __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const Stag
                     st.fx[t] = v;
                 }
             }
-            if (M.one && threadIdx.x < 125) {
+            if (M.one && st.offt && threadIdx.x < 125) {
                 const int t = threadIdx.x;
                 const double na = (double)(t / 25 - 2), nb = (double)((t / 5) % 5 - 2), nc = (double)(t % 5 - 2);
                 double o[3];
@@ -374,8 +375,8 @@ __device__ __forceinline__ void unpack_jimg(uint64_t key, int& j, int& na, int& 
 // nearest image — its only candidate image. Its image n = (s_q - s_j) - carry (s = floors, carry =
 // the wrap of W_j - W_q) and the reference arithmetic (offset from the staged 5^3 table, |n| <=
 // nref = 2) give the exact d2.
-__device__ __forceinline__ double exact_one(const StageView& st, const u32x4 fq, const u32x4 fj, int j,
-                                            const double q[3], int n[3], bool& inr) {
+__device__ __forceinline__ double exact_one(const StructMeta& M, const StageView& st, const u32x4 fq, const u32x4 fj,
+                                            int j, const double q[3], int n[3], bool& inr) {
     inr = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -386,7 +387,15 @@ __device__ __forceinline__ double exact_one(const StageView& st, const u32x4 fq,
         n[k] = (floor_of(fq.w, k) - floor_of(fj.w, k)) - carry;
         inr = inr && (uint32_t)(n[k] + 2) <= 4u;  // |n| <= nref = 2
     }
-    const f64x4 o = st.offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
+    f64x4 o;
+    if (st.offt) {
+        o = st.offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
+    } else {  // the table's arithmetic: ((na*a + nb*b) + nc*c)
+        const double na = inr ? (double)n[0] : 0.0, nb = inr ? (double)n[1] : 0.0, nc = inr ? (double)n[2] : 0.0;
+        o.x = (na * M.L[0] + nb * M.L[3]) + nc * M.L[6];
+        o.y = (na * M.L[1] + nb * M.L[4]) + nc * M.L[7];
+        o.z = (na * M.L[2] + nb * M.L[5]) + nc * M.L[8];
+    }
     const double p0 = st.x[j] + o.x, p1 = st.y[j] + o.y, p2 = st.z[j] + o.z;  // p = pos + offset
     const double e0 = q[0] - p0, e1 = q[1] - p1, e2 = q[2] - p2;
     return ((0.0 + e0 * e0) + e1 * e1) + e2 * e2;  // L2_Simple_Adaptor accumulation
@@ -458,13 +467,13 @@ __device__ __forceinline__ int count_staged_one(const StructMeta& M, const Stage
         if (ok0 && !hit0 && d2.x <= hi32) {  // borderline: the exact reference arithmetic decides
             int n[3];
             bool inr;
-            const double e2 = exact_one(st, fq, a, j0, q, n, inr);
+            const double e2 = exact_one(M, st, fq, a, j0, q, n, inr);
             hit0 = inr && e2 < rc2;
         }
         if (ok1 && !hit1 && d2.y <= hi32) {
             int n[3];
             bool inr;
-            const double e2 = exact_one(st, fq, c, j1, q, n, inr);
+            const double e2 = exact_one(M, st, fq, c, j1, q, n, inr);
             hit1 = inr && e2 < rc2;
         }
         const uint64_t bal0 = ballot(hit0), bal1 = ballot(hit1);
@@ -496,7 +505,7 @@ __device__ __forceinline__ void search_staged_one(const StructMeta& M, const Sta
         const u32x4 fj = st.fx[j];
         int n[3];
         bool inr;
-        const double d2 = exact_one(st, fq, fj, j, q, n, inr);
+        const double d2 = exact_one(M, st, fq, fj, j, q, n, inr);
         bool hit = valid && inr && d2 < rc2;         // RadiusResultSet: strict
         if (hit && j == li) hit = !(sqrt(d2) < eps);  // self skip (neighbor_list.cpp:47)
         visit(hit, j, n[0], n[1], n[2], d2);
@@ -701,7 +710,7 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
 // a bit per atom (mask[gi][kMaskWords]) so the emit and Betti passes skip the search.
 // ------------------------------------------------------------------------------------------
 #ifndef DGN_COUNT_WAVES
-#define DGN_COUNT_WAVES 4
+#define DGN_COUNT_WAVES 5
 #endif
 __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT_WAVES))) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
                                                                    int64_t* __restrict__ block_sums,
@@ -784,30 +793,51 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
                                                                   uint32_t* __restrict__ max_natoms) {
     __shared__ int64_t wtot[kScanThreads / kWave];
     __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave], wna[kScanThreads / kWave];
-    __shared__ int64_t carry_s;
     const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+    __shared__ int64_t carry_s;
     if (tid == 0) carry_s = 0;
+    // reductions of the block aux words: coalesced, independent loads
     uint64_t mx = 0, sq = 0, na = 0;
+    for (int64_t i = tid; i < n; i += kScanThreads) {
+        mx = aux[3 * i] > mx ? aux[3 * i] : mx;
+        sq += aux[3 * i + 1];
+        na = aux[3 * i + 2] > na ? aux[3 * i + 2] : na;
+    }
     __syncthreads();
-    for (int64_t base = 0; base < n; base += kScanThreads) {
-        const int64_t i = base + tid;
-        const int64_t x = i < n ? v[i] : 0;
-        if (i < n) {
-            mx = aux[3 * i] > mx ? aux[3 * i] : mx;
-            sq += aux[3 * i + 1];
-            na = aux[3 * i + 2] > na ? aux[3 * i + 2] : na;
+    // exclusive scan, 8 consecutive sums per thread (two 32-byte loads per lane: coalesced), 8192
+    // per step
+    constexpr int kPer = 8;
+    typedef int64_t i64x4 __attribute__((ext_vector_type(4)));
+    for (int64_t base = 0; base < n; base += (int64_t)kScanThreads * kPer) {
+        const int64_t i0 = base + (int64_t)tid * kPer;
+        int64_t x[kPer];
+        if (i0 + kPer <= n && (((uintptr_t)(v + i0)) & 31) == 0) {
+            const i64x4 a = *reinterpret_cast<const i64x4*>(v + i0), b = *reinterpret_cast<const i64x4*>(v + i0 + 4);
+            x[0] = a.x, x[1] = a.y, x[2] = a.z, x[3] = a.w, x[4] = b.x, x[5] = b.y, x[6] = b.z, x[7] = b.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) x[k] = i0 + k < n ? v[i0 + k] : 0;
         }
-        const int64_t inc = wave_inclusive_sum(x);
+        int64_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) tot += x[k];
+        const int64_t inc = wave_inclusive_sum(tot);
         if (lane == kWave - 1) wtot[w] = inc;
         __syncthreads();
         int64_t woff = 0;
         for (int k = 0; k < w; ++k) woff += wtot[k];
         const int64_t carry = carry_s;
-        if (i < n) v[i] = carry + woff + inc - x;
+        int64_t acc = carry + woff + inc - tot;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (i0 + k < n) v[i0 + k] = acc;
+            acc += x[k];
+        }
         __syncthreads();
-        if (tid == kScanThreads - 1) carry_s = carry + woff + inc;
+        if (tid == kScanThreads - 1) carry_s = acc;
         __syncthreads();
     }
+    if (tid == 0) *total = carry_s;
     mx = wave_max(mx);
     sq = wave_sum(sq);
     na = wave_max(na);
@@ -818,7 +848,6 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
     }
     __syncthreads();
     if (tid == 0) {
-        *total = carry_s;
         uint64_t m = 0, s = 0, a = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) {
             m = wmx[k] > m ? wmx[k] : m;
@@ -983,7 +1012,7 @@ __device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, c
 // output's 16-byte phase) and leave as non-temporal 16-byte stores.
 // ------------------------------------------------------------------------------------------
 #ifndef DGN_RBF_BUF_BYTES
-#define DGN_RBF_BUF_BYTES 4352  // per wave: 21 edges x 50 f32 bins
+#define DGN_RBF_BUF_BYTES 4352  // per wave: 21 edges x 50 f32 bins (3 lanes per edge)
 #endif
 struct RbfStreamGeom {
     int ep, seg, h;  // edges per pass, lanes per edge, bins per lane
@@ -1000,20 +1029,23 @@ __host__ __device__ inline RbfStreamGeom rbf_stream_geom(int nb, int elem) {
 __host__ __device__ inline int rbf_stream_buf_bytes(const RbfStreamGeom& gm, int nb, int elem) {
     return ((gm.ep * nb + 16 / elem) * elem + 16 + 15) / 16 * 16;
 }
-// exp(x) for |x| < 700 (no range checks): x = n ln2 + r, |r| <= ln2 / 2, Taylor of degree DEG in
-// r (DEG 12: < 2e-16 truncation; DEG 8: < 6e-9), times 2^n
+// exp(x) for |x| < 700 (no range checks): x = n ln2 + r, |r| <= ln2 / 2, Taylor polynomial of
+// degree DEG in r by Horner with the coefficients 1/k! (DEG 12: < 2e-16 truncation; DEG 8:
+// < 6e-9), times 2^n
 template <int DEG>
 __device__ __forceinline__ double exp_bounded(double x) {
+    constexpr double kInvFact[13] = {1.0, 1.0, 1.0 / 2, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040,
+                                     1.0 / 40320, 1.0 / 362880, 1.0 / 3628800, 1.0 / 39916800, 1.0 / 479001600};
     const double n = __builtin_rint(x * 1.4426950408889634);
     double r = __builtin_fma(-n, 6.93147180369123816490e-01, x);
     r = __builtin_fma(-n, 1.90821492927058770002e-10, r);
-    double p = 1.0;
+    double p = kInvFact[DEG];
 #pragma unroll
-    for (int k = DEG; k >= 1; --k) p = __builtin_fma(p, r * (1.0 / k), 1.0);
+    for (int k = DEG - 1; k >= 0; --k) p = __builtin_fma(p, r, kInvFact[k]);
     return __builtin_ldexp(p, (int)n);
 }
 template <typename T>
-__device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, const double* __restrict__ dl,
+__device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, const DGN_LDS double* dl,
                                                 const DGN_LDS double* ctab, DGN_LDS T* buf, const RbfSpec& rs,
                                                 const RbfStreamGeom gm, int w) {
     constexpr int V = 16 / sizeof(T);
@@ -1023,17 +1055,11 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
     const int k0 = sgi * gm.h;
     const int cnt0 = nb - k0 < gm.h ? nb - k0 : gm.h;
     const DGN_LDS f32x2* ctf = reinterpret_cast<const DGN_LDS f32x2*>(ctab + gm.h + 1);  // f32 (C_i, C_i+1)
-    // the next pass's distance is loaded while this pass computes and streams
-    double dnext = (w * gm.ep + le < ne && le < gm.ep) ? dl[w * gm.ep + le] : 0.0;
     for (int e = w * gm.ep; e < ne; e += kW * gm.ep) {
         const int nedge = ne - e < gm.ep ? ne - e : gm.ep;
         T* o = out + (int64_t)e * nb;
         const int phase = (int)(((uintptr_t)o / sizeof(T)) & (V - 1));  // o - phase is 16-byte aligned
-        const double d = dnext;
-        {
-            const int en = e + kW * gm.ep + le;
-            dnext = (en < ne && le < gm.ep) ? dl[en] : 0.0;
-        }
+        const double d = le < nedge ? dl[e + le] : 0.0;
         if (le < nedge && cnt0 > 0) {
             const double t0 = (double)k0 * rs.dr - d;
             const double s = rs.inv_sigma2;
@@ -1079,23 +1105,24 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
             }
         }
         wave_lds_sync();
-        // stream buf[phase, phase + nedge * nb) -> o[0, nedge * nb): lanes cover 16-byte units
+        // stream buf[phase, phase + nedge * nb) -> o[0, nedge * nb): lanes cover 16-byte units;
+        // whole units [1 or 0, nfull) without checks, the partial head / tail unit element-wise
         const int total = nedge * nb + phase;  // in units of T from the aligned base o - phase
-        const int nvec = (total + V - 1) / V;
-        for (int v = lane; v < nvec; v += kWave) {
-            const int f = V * v;
-            if (f >= phase && f + V <= total) {
-                typedef T vec_t __attribute__((ext_vector_type(V)));
-                const vec_t val = *reinterpret_cast<const DGN_LDS vec_t*>(buf + f);
+        const int v0 = phase ? 1 : 0, nfull = total / V;
+        typedef T vec_t __attribute__((ext_vector_type(V)));
+        T* ob = o - phase;
+        for (int v = v0 + lane; v < nfull; v += kWave) {
+            const vec_t val = *reinterpret_cast<const DGN_LDS vec_t*>(buf + V * v);
 #ifdef DGN_RBF_PLAIN_STORE
-                *reinterpret_cast<vec_t*>(o - phase + f) = val;
+            *reinterpret_cast<vec_t*>(ob + V * v) = val;
 #else
-                __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(o - phase + f));
+            __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(ob + V * v));
 #endif
-            } else {
-                for (int u = 0; u < V; ++u)
-                    if (f + u >= phase && f + u < total) (o - phase)[f + u] = buf[f + u];
-            }
+        }
+        if (lane < V) {
+            const int fh = lane, ft = V * nfull + lane;  // head unit 0 (phase > 0), tail unit nfull
+            if (phase && fh >= phase && fh < total) ob[fh] = buf[fh];
+            if (ft < total && ft >= phase) ob[ft] = buf[ft];
         }
         wave_lds_sync();
     }
@@ -1111,13 +1138,14 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
 // ------------------------------------------------------------------------------------------
 // Dynamic LDS of the emit (bytes): region A (search phase: stage, hit lists, hit masks, sorted
 // distances) is dead once the block's atoms are placed and is reused as region B (the per-wave
-// RBF buffers); then the RBF C table.
+// RBF buffers); then the tile's kept distances and the RBF C table, which live to the end.
 struct EmitLayout {
-    int stage, keyd, keyj, mask, sorted, rbf, ctab, total;
+    int stage, keyd, keyj, mask, sorted, dl, rbf, ctab, total;
     RbfStreamGeom gm;
     int wbytes;
 };
-__host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool stream, int nb, int elem, int nwm) {
+__host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool stream, int K, int nb, int elem,
+                                                  int nwm) {
     EmitLayout l{};
     int o = 0;
     auto take = [&](int bytes) {
@@ -1133,8 +1161,13 @@ __host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool s
     const int a_end = o;
     l.gm = rbf_stream_geom(nb > 0 ? nb : 1, elem > 0 ? elem : 4);
     l.wbytes = (stream && nb > 0) ? rbf_stream_buf_bytes(l.gm, nb, elem > 0 ? elem : 4) : 0;
+    // region B: the per-wave RBF buffers; then (live throughout) the tile's kept distances, which
+    // the rows phase leaves in LDS so the RBF phase issues no global load (a load issued after a
+    // wave's stores waits for them)
     l.rbf = 0;
-    o = a_end > kW * l.wbytes ? a_end : (kW * l.wbytes + 15) / 16 * 16;
+    const int b_end = kW * l.wbytes;
+    o = a_end > b_end ? a_end : (b_end + 15) / 16 * 16;
+    l.dl = take((stream && nb > 0) ? (kQA * K + 1) * 8 : 0);
     l.ctab = take(stream ? (l.gm.h + 1) * 8 + (l.gm.h + 2) * 4 : 0);  // f64 C_i, then f32 C_i
     l.total = o;
     return l;
@@ -1174,15 +1207,15 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                                                                   RbfSpec rs, uint32_t* __restrict__ error_flag,
                                                                   EmitTiles tl) {
     extern __shared__ double dyn[];
-    __shared__ double4 offt_s[125];
     __shared__ uint32_t ring[kW][kRing];
     __shared__ uint8_t claim[kW][kWave];
     __shared__ int64_t row_start[kQA + 1];
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
     const int elem = rs.dtype == 2 ? 8 : 4;
-    const EmitLayout ly = emit_layout(stage_cap, CAP, STREAM, rs.dtype ? rs.nbins : 0, elem, nwm);
+    const EmitLayout ly = emit_layout(stage_cap, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, elem, nwm);
     DGN_LDS uint8_t* base = reinterpret_cast<DGN_LDS uint8_t*>(lds(dyn));
-    const StageView st = make_stage(reinterpret_cast<double*>(dyn) + ly.stage / 8, stage_cap, offt_s);
+    const StageView st = make_stage(reinterpret_cast<double*>(dyn) + ly.stage / 8, stage_cap, nullptr);
+    DGN_LDS double* dl = reinterpret_cast<DGN_LDS double*>(base + ly.dl);
     DGN_LDS double* key_d = reinterpret_cast<DGN_LDS double*>(base + ly.keyd);
     DGN_LDS uint64_t* key_j = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.keyj);
     DGN_LDS uint64_t* mask_s = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.mask);
@@ -1202,7 +1235,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     uint64_t tprev = __builtin_amdgcn_s_memtime();
 #endif
     // the RBF of this tile from its rows (row_ptr, dist), by the block's 4 waves; region A must be dead
-    auto rbf_tile = [&]() __attribute__((always_inline)) {
+    auto rbf_tile = [&](bool rows_in_lds) __attribute__((always_inline)) {
         for (int i = threadIdx.x; i <= ly.gm.h + 1; i += kGraphBlock) {
             const double xx = (double)i * rs.dr;
             const double c = exp(-0.5 * (xx * xx) * rs.inv_sigma2);  // C_i
@@ -1214,17 +1247,21 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         // written by this same launch
         const int64_t e0 = row_ptr[g0], e1 = row_ptr[g0 + nq - 1] + counts[g0 + nq - 1];
         const int ne = (int)(e1 - e0);
+        if (!rows_in_lds) {  // RBF tile of an earlier launch's rows
+            for (int i = threadIdx.x; i < ne; i += kGraphBlock) dl[i] = dist[e0 + i];
+            __syncthreads();
+        }
         if (rs.dtype == 1)
-            rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dist + e0, ctab,
+            rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
                             reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
         else
-            rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dist + e0, ctab,
+            rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
                             reinterpret_cast<DGN_LDS double*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
         EMIT_STAMP(4);
     };
     if constexpr (STREAM) {
         if (is_rbf) {
-            rbf_tile();
+            rbf_tile(false);
 #ifdef DGN_EMIT_PHASES
             if (lane == 0 && (blockIdx.x & 63) == 1)
                 for (int k = 0; k < 8; ++k) atomicAdd(&dgn_emit_phase[k], (unsigned long long)ph[k]);
@@ -1279,7 +1316,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                     const int j = (int)ring[w][lane];
                     int n[3];
                     bool inr;
-                    const double d2 = exact_one(P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    const double d2 = exact_one(M, P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
                     ok = inr && d2 < g.rc2;
                     kd[lane] = sqrt(d2);  // neighbor_list.cpp:53
                     kj[lane] = pack_jimg(j, n[0], n[1], n[2]);
@@ -1328,7 +1365,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             const int64_t e = rs0 + rank;
             int j, na, nb, nc;
             unpack_jimg(key, j, na, nb, nc);
-            if constexpr (!STREAM) sd[rank] = d;
+            if constexpr (STREAM) dl[e - row_start[0]] = d;
+            else sd[rank] = d;
             col[e] = j;
             if (dist) dist[e] = d;
             if (disp) {
@@ -1368,8 +1406,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     });
     if constexpr (STREAM) {
         if (tl.fused) {
-            __syncthreads();  // the block's rows are written (visible to its waves); region A is dead
-            rbf_tile();
+            __syncthreads();  // the block's rows are in dl; region A is dead
+            rbf_tile(true);
         }
     }
 #ifdef DGN_EMIT_PHASES
@@ -1429,7 +1467,7 @@ __global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLau
                     const int j = (int)ring[w][lane];
                     int n[3];
                     bool inr;
-                    const double d2 = exact_one(P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    const double d2 = exact_one(M, P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
                     ok = inr && d2 < g.rc2;
                     key_j[w][lane] = pack_jimg(j, n[0], n[1], n[2]);
                 }
@@ -1575,7 +1613,8 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
                           void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
     const int64_t nt = graph_blocks(g.num_atoms);
     const int nwm = (stage + 63) / 64;
-    const EmitLayout ly = emit_layout(stage, CAP, STREAM, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
+    const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
+    const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
     auto go = [&](EmitTiles tl) {
         const int64_t blocks = tl.nrow + tl.nrbf;
         if (blocks > 0)
@@ -1595,6 +1634,15 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
         const char* e = getenv("DGN_EMIT_PIPELINE");
         return e && e[0] == '1';
     }();
+    static const bool split = [] {
+        const char* e = getenv("DGN_EMIT_SPLIT");
+        return e && e[0] == '1';
+    }();
+    if (split) {  // diagnostics: all rows, then all RBF (two launches)
+        go({0, nt, 0, 0, 0});
+        go({0, 0, 0, nt, 0});
+        return;
+    }
     if (!pipeline) {
         go({0, nt, 0, 0, 1});  // each block: rows, then its RBF
         return;
@@ -1630,7 +1678,11 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
                              double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
     const int64_t nb = graph_blocks(g.num_atoms);
     if (nb <= 0) return hipSuccess;
+#ifdef DGN_EMIT_FLAT
+    const bool stream = false;  // A/B diagnostics: per-atom write_rbf_flat
+#else
     const bool stream = g.kmax <= (uint64_t)kStreamMaxK;
+#endif
 #define DGN_EMIT(C)                                                                                              \
     case C:                                                                                                      \
         if (stream) launch_emit_t<C, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, \

@@ -21,7 +21,7 @@ EXPORTS = [
     "dgn_ctx_last_error", "dgn_ctx_enable_timing", "dgn_ctx_kernel_times", "dgn_ctx_reset_timing",
     "dgn_graph_params_default", "dgn_rbf_bins", "dgn_dev_graph_count", "dgn_dev_graph_emit", "dgn_host_graph",
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
-    "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds",
+    "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch",
 ]
 
@@ -108,6 +108,8 @@ def lib():
     L.dgn_host_persistence.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
     L.dgn_host_persistence_lower.argtypes = [vp, vp, vp, i64, i32, dbl, vp, i32, vp]
     L.dgn_host_rbf.argtypes = [vp, vp, i64, dbl, dbl, i32, i32, vp]
+    if hasattr(L, "dgn_dev_node_features"):  # absent from older A/B builds
+        L.dgn_dev_node_features.argtypes = [vp, C.POINTER(Batch), vp, i32, i32, vp, vp, vp, i32, vp]
     if hasattr(L, "dgn_debug_betti_clouds"):  # absent from older A/B builds
         L.dgn_debug_betti_clouds.argtypes = [vp, vp, dbl, i64, i64, i32, vp, vp, vp]
     L.dgn_synth_atoms_per_structure.restype = i64
@@ -256,6 +258,15 @@ class Context:
         self._check(lib().dgn_host_persistence_lower(self.h, _ptr(lower), _ptr(npoints), Cn, max_points, threshold,
                                                      _ptr(pairs), cap, _ptr(counts)), "dgn_host_persistence_lower")
         return pairs, counts
+
+    def dev_node_features(self, batch: dict, embed, betti, pca_mean, pca_components, out):
+        """Device tensors: embed [S][D], betti [A][35] (or None), pca_mean [35], pca_components
+        [35][k] (row-major), out [A][D + k] f64."""
+        b = make_batch(batch)
+        S, D = int(embed.shape[0]), int(embed.shape[1])
+        k = 0 if betti is None else int(pca_components.shape[1])
+        self._check(lib().dgn_dev_node_features(self.h, C.byref(b), _ptr(embed), S, D, _ptr(betti), _ptr(pca_mean),
+                                                _ptr(pca_components), k, _ptr(out)), "dgn_dev_node_features")
 
     def debug_betti_clouds(self, batch: dict, r_cutoff: float, atom_first: int, count: int, max_points: int):
         """Diagnostics: the Betti pass's local complexes of atoms [atom_first, atom_first + count):

@@ -146,6 +146,19 @@ int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* 
 int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
                    double* features, int32_t* counts);
 
+/* ---- node features + topological block (CrystalGraph node_features) --------
+ * Device pointers, asynchronous on the context's stream. out: [A][D + k] f64 row-major, row i =
+ * embed[species[i]] (the species-keyed embedding gather of crystal_graph.cpp:19-21; embed is
+ * [num_keys][D] f64 row-major, row s = atom_embeddings.at(s)) followed by k columns
+ * (betti[i] - pca_mean) * pca_components (PCA::transform, pca.cpp:36-44; betti [A][35] f64 as
+ * dgn_dev_betti writes it, pca_mean [35], pca_components [35][k] row-major, k <= 35): the
+ * N x (D + k) concatenation add_topo_features (crystal_graph.cpp:65-67) names. betti may be NULL
+ * (k must then be 0). The call waits for its stream (one flag read back) and returns DGN_ERR_ARG
+ * if a species key is outside [0, num_keys): the reference's std::map::at throws out_of_range. */
+int dgn_dev_node_features(dgn_ctx* ctx, const dgn_batch* batch, const double* embed, int32_t num_keys, int32_t D,
+                          const double* betti, const double* pca_mean, const double* pca_components, int32_t k,
+                          double* out);
+
 /* Local-complex persistence from point clouds (replaces topology::compute_persistence,
  * src/topology/ripser_wrapper.cpp:60-70). clouds: [C][max_points][3] f64 (host), npoints[C].
  * pairs: [C][3][cap][2] f32 (host) sorted ascending by (birth, death); counts [C][4]. */
