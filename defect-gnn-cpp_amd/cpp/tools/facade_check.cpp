@@ -5,6 +5,8 @@
 //   facade_check pca <features.bin> <n_components> <out.txt>        (host: load_betti_features + PCA)
 #include <cmath>
 #include <cstdio>
+#include <fstream>
+#include <sstream>
 #include <limits>
 #include <map>
 #include <string>
@@ -18,6 +20,7 @@
 #include "topology/betti_features.hpp"
 #include "topology/pca.hpp"
 #include "topology/ripser_wrapper.hpp"
+#include "viz/wasm_api.hpp"
 
 using namespace defect_gnn;
 
@@ -74,7 +77,45 @@ static int host_modes(int argc, char** argv) {
     return -1;
 }
 
+// facade_check wasm <poscar> <r_cutoff> <max_neighbors> <out.txt>: viz::WasmAPI end to end (GPU)
+static int wasm_mode(char** argv) {
+    std::ifstream in(argv[2]);
+    if (!in) return 3;
+    std::stringstream ss;
+    ss << in.rdbuf();
+    viz::WasmAPI api;
+    if (!api.load_structure(ss.str())) return 4;
+    viz::WasmAPI empty;
+    empty.build_graph(5.0, 20);  // no structure: no-op, empty accessors
+    if (empty.num_edges() != 0 || !empty.get_positions().empty() || empty.load_structure("garbage\nx\n")) return 5;
+    api.build_graph(std::stod(argv[3]), static_cast<size_t>(std::stoul(argv[4])));
+    FILE* f = std::fopen(argv[5], "w");
+    if (!f) return 3;
+    auto fl = [](const std::vector<float>& v) { return std::vector<double>(v.begin(), v.end()); };
+    auto in_ = [](const std::vector<int>& v) { return std::vector<double>(v.begin(), v.end()); };
+    dump(f, "num_atoms", {static_cast<double>(api.num_atoms())});
+    dump(f, "num_edges", {static_cast<double>(api.num_edges())});
+    dump(f, "positions", fl(api.get_positions()));
+    dump(f, "lattice", fl(api.get_lattice_vectors()));
+    dump(f, "atom_types", in_(api.get_atom_types()));
+    dump(f, "element_counts", in_(api.get_element_counts()));
+    dump(f, "sources", in_(api.get_edge_sources()));
+    dump(f, "targets", in_(api.get_edge_targets()));
+    dump(f, "distances", fl(api.get_edge_distances()));
+    dump(f, "displacements", fl(api.get_edge_displacements()));
+    std::fclose(f);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 6 && std::string(argv[1]) == "wasm") {
+        try {
+            return wasm_mode(argv);
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "facade_check: %s\n", e.what());
+            return 1;
+        }
+    }
     if (argc >= 2 && (std::string(argv[1]) == "parse" || std::string(argv[1]) == "pca")) {
         try {
             const int rc = host_modes(argc, argv);

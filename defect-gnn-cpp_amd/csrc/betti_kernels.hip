@@ -62,6 +62,7 @@ constexpr uint32_t kErrPiv = 1u << 3;
 constexpr uint32_t kErrPairs = 1u << 4;
 constexpr uint32_t kErrR = 1u << 5;
 [[maybe_unused]] constexpr uint32_t kErrOrder = 1u << 6;  // -DDGN_ORDER_CHECK builds
+constexpr uint32_t kErrCapacity = kErrWorkCol | kErrNA | kErrPiv | kErrPairs | kErrR;
 
 // scratch layout per wave (bytes)
 struct ScratchLayout {
@@ -1036,26 +1037,32 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
-            if (cx.err) {
-                if (lane == 0) atomicOr(bl.error_flag, cx.err);
+            if (bl.force_retry) cx.err |= kErrNA;
+            const uint32_t err = uni(cx.err);
+            if (err && bl.retry_list && (err & kErrCapacity) == err) {
+                // workspace overflow: the capacity-retry launch (betti_wide_kernel, big layout)
+                // reduces this complex again and writes its outputs
+                if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+            } else if (err) {
+                if (lane == 0) atomicOr(bl.error_flag, err);
                 if (feat && lane < 35) feat[lane] = __builtin_nan("");
                 if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
-                continue;
-            }
-            // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
-            const double myval = betti_stats35(s.d0, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
-            if (feat && lane < 35) feat[lane] = myval;
-            if (bl.pairs_out) {
-                float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;
-                for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, s.d0[i]);
-                for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) po[bl.pair_cap + i] = cx.pairs(1)[i];
-                for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) po[2 * bl.pair_cap + i] = cx.pairs(2)[i];
-            }
-            if (bl.counts && lane == 0) {
-                bl.counts[4 * gi + 0] = cx.n_d0;
-                bl.counts[4 * gi + 1] = cx.n_inf0;
-                bl.counts[4 * gi + 2] = cx.n_p1;
-                bl.counts[4 * gi + 3] = cx.n_p2;
+            } else {
+                // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
+                const double myval = betti_stats35(s.d0, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
+                if (feat && lane < 35) feat[lane] = myval;
+                if (bl.pairs_out) {
+                    float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;
+                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, s.d0[i]);
+                    for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) po[bl.pair_cap + i] = cx.pairs(1)[i];
+                    for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) po[2 * bl.pair_cap + i] = cx.pairs(2)[i];
+                }
+                if (bl.counts && lane == 0) {
+                    bl.counts[4 * gi + 0] = cx.n_d0;
+                    bl.counts[4 * gi + 1] = cx.n_inf0;
+                    bl.counts[4 * gi + 2] = cx.n_p1;
+                    bl.counts[4 * gi + 3] = cx.n_p2;
+                }
             }
             lds_sync();
             DGN_PHASE(6);

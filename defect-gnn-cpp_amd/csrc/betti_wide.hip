@@ -22,6 +22,8 @@
 // lane-parallel, the rest reduced in Ripser's column order (decreasing F-key); death > birth
 // only, essential dim >= 1 classes are not emitted (ripser.cpp:1209-1225, 1240). The pairing
 // of a total order is unique, so the emitted multiset equals Ripser's.
+#include <algorithm>
+
 #include "dgn_internal.hpp"
 
 namespace dgn {
@@ -32,10 +34,13 @@ constexpr uint64_t kInfW = ~0ull;
 constexpr uint32_t kNoneW = 0xFFFFFFFFu;
 constexpr uint16_t kMcNoneW = 0xFFFF;     // not a column, or no cofacet
 constexpr uint16_t kMcClearedW = 0xFFFE;  // triangle is the pivot of a dim-1 column (clearing)
-constexpr uint32_t kLazyW = 0x80000000u;  // pivot meta: V = {column simplex} (packed, low bits)
+constexpr uint64_t kLazyW = 1ull << 63;    // pivot meta: V = {column simplex} (packed, low bits)
+constexpr uint64_t kNoMetaW = ~0ull;       // pivot not in the table
+constexpr int kMetaLenBits = 24;           // pivot meta: (V-store offset << 24) | V length
 // error bits (decoded in dgn_api.cpp)
 constexpr uint32_t kEPoints = 1u << 0, kEWork = 1u << 1, kENA = 1u << 2, kEPiv = 1u << 3, kEPairs = 1u << 4,
                    kER = 1u << 5, kEGuard = 1u << 7;
+constexpr uint32_t kECapacity = kEWork | kENA | kEPiv | kEPairs | kER | kEGuard;
 
 __device__ __forceinline__ uint64_t bin2(uint64_t v) { return v * (v - 1) / 2; }
 __device__ __forceinline__ uint64_t bin3(uint64_t v) { return v * (v - 1) * (v - 2) / 6; }
@@ -442,10 +447,10 @@ struct WideCx {
         k ^= k >> 33;
         return (uint32_t)k;
     }
-    __device__ uint32_t hfind(uint64_t k) const {
+    __device__ uint64_t hfind(uint64_t k) const {
         const int lane = lane_id();
         const uint64_t* HK = sp<uint64_t>(ly.h_key);
-        const uint32_t* HM = sp<uint32_t>(ly.h_meta);
+        const uint64_t* HM = sp<uint64_t>(ly.h_meta);
         const uint32_t mask = (uint32_t)ly.h_cap - 1u;
         const uint32_t base = hmix(k) & mask;
         for (int probe = 0; probe < ly.h_cap; probe += kWave) {
@@ -453,15 +458,15 @@ struct WideCx {
             const uint64_t hit = ballot(x == k), emp = ballot(x == 0ull);
             const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
             const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
-            if (fh < fe) return uniw(HM[(base + (uint32_t)(probe + fh)) & mask]);
-            if (fe < kWave) return kNoneW;
+            if (fh < fe) return uniw64(HM[(base + (uint32_t)(probe + fh)) & mask]);
+            if (fe < kWave) return kNoMetaW;
         }
-        return kNoneW;
+        return kNoMetaW;
     }
-    __device__ bool hinsert(uint64_t k, uint32_t meta, int npiv) {
+    __device__ bool hinsert(uint64_t k, uint64_t meta, int npiv) {
         const int lane = lane_id();
         uint64_t* HK = sp<uint64_t>(ly.h_key);
-        uint32_t* HM = sp<uint32_t>(ly.h_meta);
+        uint64_t* HM = sp<uint64_t>(ly.h_meta);
         const uint32_t mask = (uint32_t)ly.h_cap - 1u;
         const uint32_t base = hmix(k) & mask;
         if (npiv >= ly.na_cap) return false;
@@ -631,29 +636,31 @@ struct WideCx {
         uint32_t* vstore = sp<uint32_t>(ly.vstore);
         float2* pairs = sp<float2>(dim == 1 ? ly.p1 : ly.p2);
         int& np = dim == 1 ? n_p1 : n_p2;
-        int npiv = 0, vused = 0;
+        int npiv = 0;
+        int64_t vused = 0;
         for (int ci = 0; ci < nna && err == 0u; ++ci) {
             const uint64_t colkey = uniw64(K[ci]);
             uint64_t tau = uniw64(T[ci]);
             uint64_t tv = uniw64(V[ci]);
             const uint32_t cp = uniw(Cc[ci]);
             const uint32_t birth = (uint32_t)(colkey >> 32);
-            uint32_t meta = hfind(tau);
+            uint64_t meta = hfind(tau);
             WSUB(1);
-            uint32_t app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+            uint32_t app = meta == kNoMetaW ? apparent_owner(dim, tv) : kNoneW;
             WSUB(2);
             int v = 0;  // 0 = lazy: V == {this column}
-            if (meta != kNoneW || app != kNoneW) {
+            if (meta != kNoMetaW || app != kNoneW) {
                 v_toggle(cp, v);
-                long guard = 0;
+                int64_t guard = 0;
                 for (;;) {
                     bool ok = true;
                     if (app != kNoneW) {
                         ok = v_toggle(app, v);
                     } else if (meta & kLazyW) {
-                        ok = v_toggle(meta & ~kLazyW, v);
+                        ok = v_toggle((uint32_t)(meta & ~kLazyW), v);
                     } else {
-                        const int off = (int)(meta >> 10), len = (int)(meta & 1023u);
+                        const int64_t off = (int64_t)(meta >> kMetaLenBits);
+                        const int len = (int)(meta & ((1ull << kMetaLenBits) - 1));
                         for (int t0 = 0; t0 < len && ok; t0 += kWave) {
                             const uint32_t w = t0 + lane < len ? vstore[off + t0 + lane] : 0u;
                             const int cnt = len - t0 < kWave ? len - t0 : kWave;
@@ -672,10 +679,10 @@ struct WideCx {
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
                     meta = hfind(tau);
                     WSUB(1);
-                    app = meta == kNoneW ? apparent_owner(dim, tv) : kNoneW;
+                    app = meta == kNoMetaW ? apparent_owner(dim, tv) : kNoneW;
                     WSUB(2);
-                    if (meta == kNoneW && app == kNoneW) break;  // tau is this column's pivot
-                    if (++guard > (1l << 20)) {
+                    if (meta == kNoMetaW && app == kNoneW) break;  // tau is this column's pivot
+                    if (++guard > ly.guard) {
                         err |= kEGuard;
                         break;
                     }
@@ -688,18 +695,18 @@ struct WideCx {
                 ++np;
             }
             if (dim == 1 && lane == 0) sp<uint16_t>(ly.mc_t)[pidx(3, tv)] = kMcClearedW;  // clearing
-            uint32_t m;
+            uint64_t m;
             if (v == 0) {
                 m = kLazyW | cp;
             } else {
-                if (vused + v > ly.vs_cap || v > 1023) {
+                if ((int64_t)vused + v > ly.vs_cap) {
                     err |= kER;
                     break;
                 }
                 const uint32_t* VL = sp<uint32_t>(ly.vlist);
                 for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
                 __syncthreads();
-                m = ((uint32_t)vused << 10) | (uint32_t)v;
+                m = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;
             }
             if (!hinsert(tau, m, npiv)) {
@@ -731,6 +738,13 @@ struct WideCx {
         const int lane = lane_id();
         double* feat = bl.features ? bl.features + 35 * gi : nullptr;
         if (n_p1 > ly.p_cap || n_p2 > ly.p_cap) err |= kEPairs;
+        if (bl.force_retry && bl.retry_list) err |= kENA;
+        if (err && bl.retry_list && (err & kECapacity) == err) {
+            // workspace overflow: listed for the capacity-retry launch (betti_wide_layout big),
+            // which writes this complex's outputs
+            if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+            return;
+        }
         if (err) {
             if (lane == 0) atomicOr(bl.error_flag, err);
             if (feat && lane < 35) feat[lane] = __builtin_nan("");
@@ -847,18 +861,22 @@ size_t wide_lds_bytes(int nmax) {
 }  // namespace
 
 // Scratch layout of one wave for complexes of up to nmax points (all offsets 256-B aligned).
-WideLayout betti_wide_layout(int nmax) {
+// big = the capacity-retry layout (complexes whose reduction outgrew the regular caps): column,
+// pivot and pair tables sized for every simplex of the complex, a 16M-entry V store.
+WideLayout betti_wide_layout(int nmax, bool big) {
     WideLayout l{};
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
     int64_t cap = 1024;
-    while (cap < t && cap < (int64_t(1) << 17)) cap <<= 1;
+    const int64_t cap_max = big ? (int64_t(1) << 30) : (int64_t(1) << 17);
+    while ((cap < t || cap < e) && cap < cap_max) cap <<= 1;
     l.nmax = nmax;
     l.na_cap = (int32_t)cap;
     l.p_cap = (int32_t)cap;
     l.h_cap = (int32_t)(2 * cap);
-    l.vs_cap = 1 << 20;
-    l.vl_cap = 1 << 16;
+    l.vs_cap = big ? (1 << 24) : (1 << 20);
+    l.vl_cap = big ? (int32_t)std::min<int64_t>(cap, 1 << 22) : (1 << 16);
+    l.guard = big ? (int64_t(1) << 32) : (int64_t(1) << 20);
     int64_t o = 0;
     auto take = [&](int64_t bytes) {
         const int64_t at = o;
@@ -877,7 +895,7 @@ WideLayout betti_wide_layout(int nmax) {
     l.vlist = take(4 * (int64_t)l.vl_cap);
     l.vdiam = take(4 * (int64_t)l.vl_cap);
     l.h_key = take(8 * 2 * cap);
-    l.h_meta = take(4 * 2 * cap);
+    l.h_meta = take(8 * 2 * cap);
     l.h_used = take(4 * cap);
     l.p1 = take(8 * cap);
     l.p2 = take(8 * cap);

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -71,7 +72,9 @@ struct Scalars {  // device-side scalars, one allocation
     uint32_t overflow_len;      // complexes routed to the overflow launch
     uint32_t wide_queue;        // betti wide launch queue
     uint32_t wide_len;          // complexes routed to the wide launch
-    uint32_t pad[1];
+    uint32_t retry_len;         // complexes routed to the capacity-retry launch
+    uint32_t retry_queue;       // capacity-retry launch queue
+    uint32_t pad[2];
 };
 
 // one neighbour pass's device workspace and the facts its count recorded (count -> emit handshake)
@@ -109,7 +112,7 @@ struct dgn_ctx {
     HostScalars* host = nullptr;  // pinned
     bool emit_pending = false;    // an emit's error flag is on its way to host->emit_flag
     // betti workspace
-    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide;
+    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big;
     int betti_slots = 0;
     bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
@@ -399,6 +402,10 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
         const int64_t resident = betti_wide_resident_waves(c->device, max_points);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
+        if (const char* ev = std::getenv("DGN_WIDE_WAVES")) {  // A/B experiments only
+            const int w = std::atoi(ev);
+            if (w > 0 && w < wide_waves) wide_waves = w;
+        }
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
@@ -433,6 +440,10 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.wide_list = max_points > 64 ? c->b_wlist.as<int32_t>() : nullptr;
     bl.wide_len = &sc->wide_len;
     bl.wide_queue = &sc->wide_queue;
+    HIP_TRY(c, c->b_rlist.ensure(sizeof(int32_t) * (size_t)A));
+    bl.retry_list = c->b_rlist.as<int32_t>();
+    bl.retry_len = &sc->retry_len;
+    if (const char* fr = std::getenv("DGN_FORCE_RETRY")) bl.force_retry = std::atoi(fr) != 0;  // tests only
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, c->phase.ensure(32 * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
@@ -450,10 +461,44 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.features = features ? features + 35 * c0 : nullptr;
         pb.counts = counts ? counts + 4 * c0 : nullptr;
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
-        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 5 * sizeof(uint32_t), c->stream));
-        TimedLaunch t(c, "betti_vr", bytes, 0.0);
-        HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr, wide_waves,
-                                &fork));
+        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 7 * sizeof(uint32_t), c->stream));
+        {
+            TimedLaunch t(c, "betti_vr", bytes, 0.0);
+            HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr,
+                                    wide_waves, &fork));
+        }
+        // complexes whose reduction outgrew a kernel's workspace (the reference's Ripser has no
+        // caps, ripser.cpp:514-1269): reduced again with the big wide layout
+        HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        const int64_t nretry = c->host->s.retry_len;
+        if (nretry == 0) return DGN_OK;
+        const int nmax = std::max(max_points, 64);
+        WideLayout big = betti_wide_layout(nmax, true);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        const int64_t budget = (int64_t)(free_b / 2) + (int64_t)c->b_big.bytes;
+        const int64_t waves = std::min<int64_t>({nretry, budget / big.total, betti_wide_resident_waves(c->device, nmax)});
+        if (waves < 1)
+            return fail(c, DGN_ERR_CAPACITY, "capacity retry: no device memory for a " + std::to_string(big.total) +
+                                                 "-byte workspace");
+        HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
+        big.base = c->b_big.as<uint8_t>();
+        HIP_TRY(c, betti_wide_init_scratch(c->stream, big, (int)waves));
+        BettiLaunch rb = pb;
+        rb.wide_list = c->b_rlist.as<int32_t>();
+        rb.wide_len = &sc->retry_len;
+        rb.wide_queue = &sc->retry_queue;
+        rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
+        rb.retry_len = nullptr;
+        rb.force_retry = 0;
+        {
+            TimedLaunch t(c, "betti_retry", 0.0, 0.0);
+            HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)waves));
+        }
+        // the regular wide layout's tables are not touched; the big buffer is kept for reuse
+        HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
         return DGN_OK;
     };
     // triangles: floats per complex, padded to a multiple of 4 (16-byte aligned complexes)
@@ -787,6 +832,85 @@ int dgn_dev_node_features(dgn_ctx* c, const dgn_batch* b, const double* embed, i
     if (c->host->s.error_flag)
         return fail(c, DGN_ERR_ARG, "dgn_dev_node_features: a species key has no embedding row (atom_embeddings.at)");
     return DGN_OK;
+}
+
+int dgn_dev_edge_arrays(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, const int32_t* col_idx,
+                        const double* distance, const double* displacement, int32_t* sources, int32_t* targets,
+                        float* distances_f32, float* displacements_f32) {
+    if (!c || !batch_ok(b) || !row_ptr || (targets && !col_idx) || (distances_f32 && !distance) ||
+        (displacements_f32 && !displacement))
+        return fail(c, DGN_ERR_ARG, "dgn_dev_edge_arrays: bad args");
+    if (b->num_atoms == 0) return DGN_OK;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const double A = (double)b->num_atoms;
+    TimedLaunch t(c, "edge_arrays", 8 * (A + 1), 0.0);  // + per edge: in 4 + 8 + 24 B, out 4 + 4 + 4 + 12 B
+    HIP_TRY(c, launch_edge_arrays(c->stream, row_ptr, b->atom_offset, b->num_structures, b->num_atoms, col_idx, distance,
+                                  displacement, sources, targets, distances_f32, displacements_f32));
+    return DGN_OK;
+}
+
+int dgn_host_edge_arrays(dgn_ctx* c, const dgn_batch* h, double r_cutoff, uint64_t max_neighbors, double epsilon,
+                         dgn_edge_arrays** out) {
+    if (!c || !out) return fail(c, DGN_ERR_ARG, "dgn_host_edge_arrays: bad args");
+    *out = nullptr;
+    HIP_TRY(c, hipSetDevice(c->device));
+    dgn_batch d;
+    int st = stage_batch(c, h, &d);
+    if (st) return st;
+    dgn_graph_params p;
+    dgn_graph_params_default(&p);
+    p.r_cutoff = r_cutoff;
+    p.max_neighbors = max_neighbors;
+    p.epsilon = epsilon;
+    p.rbf_dtype = DGN_NONE;
+    p.write_displacement = 1;
+    int64_t E = 0;
+    if ((st = dgn_dev_graph_count(c, &d, &p, &E))) return st;
+    const int64_t A = h->num_atoms, Em = std::max<int64_t>(E, 1);
+    DevBuf rp, col, dist, disp, src, tgt, d32, p32;
+    HIP_TRY(c, rp.ensure(8 * (A + 1)));
+    HIP_TRY(c, col.ensure(4 * Em));
+    HIP_TRY(c, dist.ensure(8 * Em));
+    HIP_TRY(c, disp.ensure(24 * Em));
+    HIP_TRY(c, src.ensure(4 * Em));
+    HIP_TRY(c, tgt.ensure(4 * Em));
+    HIP_TRY(c, d32.ensure(4 * Em));
+    HIP_TRY(c, p32.ensure(12 * Em));
+    if (A == 0) HIP_TRY(c, hipMemsetAsync(rp.p, 0, 8, c->stream));
+    dgn_graph_out o{col.as<int32_t>(), dist.as<double>(), disp.as<double>(), nullptr};
+    if ((st = dgn_dev_graph_emit(c, &d, &p, rp.as<int64_t>(), &o)) || (st = check_emit_flag(c))) return st;
+    if ((st = dgn_dev_edge_arrays(c, &d, rp.as<int64_t>(), col.as<int32_t>(), dist.as<double>(), disp.as<double>(),
+                                  src.as<int32_t>(), tgt.as<int32_t>(), d32.as<float>(), p32.as<float>())))
+        return st;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    dgn_edge_arrays* r = new dgn_edge_arrays();
+    r->num_edges = E;
+    r->sources = new int32_t[Em];
+    r->targets = new int32_t[Em];
+    r->distances = new float[Em];
+    r->displacements = new float[3 * Em];
+    hipError_t e = hipSuccess;
+    if (E) {
+        if (!e) e = hipMemcpy(r->sources, src.p, 4 * E, hipMemcpyDeviceToHost);
+        if (!e) e = hipMemcpy(r->targets, tgt.p, 4 * E, hipMemcpyDeviceToHost);
+        if (!e) e = hipMemcpy(r->distances, d32.p, 4 * E, hipMemcpyDeviceToHost);
+        if (!e) e = hipMemcpy(r->displacements, p32.p, 12 * E, hipMemcpyDeviceToHost);
+    }
+    if (e) {
+        dgn_edge_arrays_free(r);
+        return hip_fail(c, e, "dgn_host_edge_arrays: copy back");
+    }
+    *out = r;
+    return DGN_OK;
+}
+
+void dgn_edge_arrays_free(dgn_edge_arrays* a) {
+    if (!a) return;
+    delete[] a->sources;
+    delete[] a->targets;
+    delete[] a->distances;
+    delete[] a->displacements;
+    delete a;
 }
 
 int dgn_host_betti(dgn_ctx* c, const dgn_batch* h, const dgn_betti_params* p, double* features, int32_t* counts) {

@@ -108,6 +108,11 @@ struct BettiLaunch {
     const int32_t* work_list; // null = all complexes 0..num_atoms-1
     uint32_t* queue;          // work counter of this launch
     int32_t skip_above;       // 1 = complexes above NP are left to the overflow launch
+    // capacity retry: complexes whose reduction outgrew a kernel's workspace are appended here
+    // (null = report DGN_ERR_CAPACITY) and reduced again by betti_wide_kernel with the big layout
+    int32_t* retry_list;      // [num_atoms]
+    uint32_t* retry_len;
+    int32_t force_retry;      // tests (DGN_FORCE_RETRY=1): every narrow/wide complex takes the retry path
 };
 // wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout
 constexpr int kWideMaxPoints = 512;
@@ -115,9 +120,10 @@ struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
     int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
+    int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
     int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2, d0;
 };
-WideLayout betti_wide_layout(int nmax);
+WideLayout betti_wide_layout(int nmax, bool big = false);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax);  // device-wide resident waves (occupancy API)
 
@@ -162,5 +168,10 @@ hipError_t launch_betti(hipStream_t s, const BettiLaunch& b, int max_points, int
 hipError_t launch_node_features(hipStream_t s, const int32_t* species, int64_t A, const double* embed, int32_t nkeys,
                                 int32_t D, const double* betti, const double* mean, const double* comp, int32_t k,
                                 double* out, uint32_t* error_flag);
+// flat per-edge arrays of a CSR (WasmAPI graph accessors): src = row atom's in-structure index,
+// tgt = col, f32 casts of dist and disp [E][3]; any output may be null
+hipError_t launch_edge_arrays(hipStream_t s, const int64_t* row_ptr, const int64_t* atom_offset, int64_t B, int64_t A,
+                              const int32_t* col, const double* dist, const double* disp, int32_t* src, int32_t* tgt,
+                              float* dist32, float* disp32);
 
 }  // namespace dgn

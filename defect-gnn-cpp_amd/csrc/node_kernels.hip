@@ -76,3 +76,69 @@ hipError_t launch_node_features(hipStream_t s, const int32_t* species, int64_t A
 }
 
 }  // namespace dgn
+
+namespace dgn {
+
+// Flat per-edge arrays of a CSR, the WasmAPI graph accessors (reference src/viz/wasm_bindings.cpp:
+// 206-294: get_edge_sources / get_edge_targets / get_edge_distances / get_edge_displacements,
+// float32 casts of Neighbor::distance / displacement, sources = the row atom's index within its
+// structure). One block per 256 atom rows: the rows' CSR offsets and in-structure indices are
+// staged in LDS, then the block's contiguous edge range is written edge-parallel (coalesced).
+// HBM-bound: per edge 4 (col) + 8 (dist) + 24 (disp) B in, 4 + 4 + 4 + 12 B out.
+constexpr int kEdgeRows = 256;
+
+__global__ __launch_bounds__(kEdgeRows) void edge_arrays_kernel(const int64_t* __restrict__ row_ptr,
+                                                                 const int64_t* __restrict__ atom_offset, int64_t B,
+                                                                 int64_t A, const int32_t* __restrict__ col,
+                                                                 const double* __restrict__ dist,
+                                                                 const double* __restrict__ disp,
+                                                                 int32_t* __restrict__ src, int32_t* __restrict__ tgt,
+                                                                 float* __restrict__ dist32,
+                                                                 float* __restrict__ disp32) {
+    __shared__ int64_t rp_s[kEdgeRows + 1];
+    __shared__ int32_t local_s[kEdgeRows];
+    const int64_t a0 = (int64_t)blockIdx.x * kEdgeRows;
+    const int na = (int)(A - a0 < kEdgeRows ? A - a0 : kEdgeRows);
+    const int t = threadIdx.x;
+    if (t <= na) rp_s[t] = row_ptr[a0 + t];
+    if (t < na && src) {
+        // structure of atom a0 + t: the last s with atom_offset[s] <= a (binary search)
+        const int64_t a = a0 + t;
+        int64_t lo = 0, hi = B - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (atom_offset[mid] <= a) lo = mid;
+            else hi = mid - 1;
+        }
+        local_s[t] = (int32_t)(a - atom_offset[lo]);
+    }
+    __syncthreads();
+    const int64_t e0 = rp_s[0], e1 = rp_s[na];
+    for (int64_t e = e0 + t; e < e1; e += kEdgeRows) {
+        if (src) {
+            int lo = 0, hi = na - 1;  // row r: rp_s[r] <= e < rp_s[r + 1]
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (rp_s[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            src[e] = local_s[lo];
+        }
+        if (tgt) tgt[e] = col[e];
+        if (dist32) dist32[e] = (float)dist[e];
+    }
+    if (disp32)
+        for (int64_t x = 3 * e0 + t; x < 3 * e1; x += kEdgeRows) disp32[x] = (float)disp[x];
+}
+
+hipError_t launch_edge_arrays(hipStream_t s, const int64_t* row_ptr, const int64_t* atom_offset, int64_t B, int64_t A,
+                              const int32_t* col, const double* dist, const double* disp, int32_t* src, int32_t* tgt,
+                              float* dist32, float* disp32) {
+    if (A <= 0) return hipSuccess;
+    const int64_t nb = (A + kEdgeRows - 1) / kEdgeRows;
+    hipLaunchKernelGGL(edge_arrays_kernel, dim3((unsigned)nb), dim3(kEdgeRows), 0, s, row_ptr, atom_offset, B, A, col,
+                       dist, disp, src, tgt, dist32, disp32);
+    return hipGetLastError();
+}
+
+}  // namespace dgn

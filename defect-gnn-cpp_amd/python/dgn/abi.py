@@ -22,6 +22,7 @@ EXPORTS = [
     "dgn_graph_params_default", "dgn_rbf_bins", "dgn_dev_graph_count", "dgn_dev_graph_emit", "dgn_host_graph",
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
+    "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch",
 ]
 
@@ -57,6 +58,11 @@ class GraphResult(C.Structure):
 
 class BettiParams(C.Structure):
     _fields_ = [("r_cutoff", C.c_double)]
+
+
+class EdgeArrays(C.Structure):
+    _fields_ = [("num_edges", C.c_int64), ("sources", C.POINTER(C.c_int32)), ("targets", C.POINTER(C.c_int32)),
+                ("distances", C.POINTER(C.c_float)), ("displacements", C.POINTER(C.c_float))]
 
 
 class KernelTime(C.Structure):
@@ -110,6 +116,11 @@ def lib():
     L.dgn_host_rbf.argtypes = [vp, vp, i64, dbl, dbl, i32, i32, vp]
     if hasattr(L, "dgn_dev_node_features"):  # absent from older A/B builds
         L.dgn_dev_node_features.argtypes = [vp, C.POINTER(Batch), vp, i32, i32, vp, vp, vp, i32, vp]
+    if hasattr(L, "dgn_dev_edge_arrays"):  # absent from older A/B builds
+        L.dgn_dev_edge_arrays.argtypes = [vp, C.POINTER(Batch), vp, vp, vp, vp, vp, vp, vp, vp]
+        L.dgn_host_edge_arrays.argtypes = [vp, C.POINTER(Batch), dbl, C.c_uint64, dbl, C.POINTER(C.POINTER(EdgeArrays))]
+        L.dgn_edge_arrays_free.argtypes = [C.POINTER(EdgeArrays)]
+        L.dgn_edge_arrays_free.restype = None
     if hasattr(L, "dgn_debug_betti_clouds"):  # absent from older A/B builds
         L.dgn_debug_betti_clouds.argtypes = [vp, vp, dbl, i64, i64, i32, vp, vp, vp]
     L.dgn_synth_atoms_per_structure.restype = i64
@@ -279,6 +290,26 @@ class Context:
         self._check(lib().dgn_debug_betti_clouds(self.h, C.byref(b), r_cutoff, atom_first, count, max_points,
                                                  _ptr(lower), _ptr(npoints), _ptr(keys)), "dgn_debug_betti_clouds")
         return lower, npoints, keys
+
+    def host_edge_arrays(self, batch: dict, r_cutoff=10.0, max_neighbors=20, epsilon=1e-10):
+        """WasmAPI::build_graph + graph accessors: (sources, targets, distances f32, displacements f32 [E][3])."""
+        b = make_batch(batch)
+        res = C.POINTER(EdgeArrays)()
+        self._check(lib().dgn_host_edge_arrays(self.h, C.byref(b), r_cutoff, max_neighbors, epsilon, C.byref(res)),
+                    "dgn_host_edge_arrays")
+        r = res.contents
+        E, m = r.num_edges, max(r.num_edges, 1)
+        out = (np.ctypeslib.as_array(r.sources, (m,))[:E].copy(), np.ctypeslib.as_array(r.targets, (m,))[:E].copy(),
+               np.ctypeslib.as_array(r.distances, (m,))[:E].copy(),
+               np.ctypeslib.as_array(r.displacements, (3 * m,))[:3 * E].reshape(E, 3).copy())
+        lib().dgn_edge_arrays_free(res)
+        return out
+
+    def dev_edge_arrays(self, batch: dict, row_ptr, col, dist, disp, sources, targets, dist32, disp32):
+        b = make_batch(batch)
+        self._check(lib().dgn_dev_edge_arrays(self.h, C.byref(b), _ptr(row_ptr), _ptr(col), _ptr(dist), _ptr(disp),
+                                              _ptr(sources), _ptr(targets), _ptr(dist32), _ptr(disp32)),
+                    "dgn_dev_edge_arrays")
 
     def host_rbf(self, distances, rbf_cutoff=10.0, rbf_dr=0.1, dtype=DGN_F64, layout=0):
         d = np.ascontiguousarray(distances, dtype=np.float64)

@@ -159,6 +159,30 @@ int dgn_dev_node_features(dgn_ctx* ctx, const dgn_batch* batch, const double* em
                           const double* betti, const double* pca_mean, const double* pca_components, int32_t k,
                           double* out);
 
+/* ---- flat float32 edge arrays (WasmAPI graph accessors) ------------------
+ * Replaces WasmAPI::num_edges / get_edge_sources / get_edge_targets / get_edge_distances /
+ * get_edge_displacements (src/viz/wasm_bindings.cpp:206-294) for a whole batch: from a CSR written by
+ * dgn_dev_graph_emit (row_ptr [A+1], col_idx [E], distance [E], displacement [E][3] when requested)
+ * write sources[E] (the row atom's index within its structure), targets[E] (= col_idx),
+ * distances_f32[E] and displacements_f32[E][3] (static_cast<float> of the f64 values). Device
+ * pointers, asynchronous on the context's stream; any output may be NULL (its input may then be
+ * NULL too). */
+int dgn_dev_edge_arrays(dgn_ctx* ctx, const dgn_batch* batch, const int64_t* row_ptr, const int32_t* col_idx,
+                        const double* distance, const double* displacement, int32_t* sources, int32_t* targets,
+                        float* distances_f32, float* displacements_f32);
+/* Host-level: NeighborList(r_cutoff, max_neighbors, epsilon) of a host batch on the device, then the
+ * arrays above (WasmAPI::build_graph + the graph accessors). Free with dgn_edge_arrays_free. */
+typedef struct {
+    int64_t num_edges;
+    int32_t* sources;
+    int32_t* targets;
+    float* distances;
+    float* displacements; /* [E][3] */
+} dgn_edge_arrays;
+int dgn_host_edge_arrays(dgn_ctx* ctx, const dgn_batch* host_batch, double r_cutoff, uint64_t max_neighbors,
+                         double epsilon, dgn_edge_arrays** out);
+void dgn_edge_arrays_free(dgn_edge_arrays* a);
+
 /* Local-complex persistence from point clouds (replaces topology::compute_persistence,
  * src/topology/ripser_wrapper.cpp:60-70). clouds: [C][max_points][3] f64 (host), npoints[C].
  * pairs: [C][3][cap][2] f32 (host) sorted ascending by (birth, death); counts [C][4]. */

@@ -1,0 +1,75 @@
+"""Envelope of the Betti reduction vs the reference's verbatim vendored Ripser (oracle/_ref), which
+has no workspace caps (third_party/ripser/ripser.cpp:514-1269): complexes whose reduction outgrows
+a kernel's per-wave workspace (cliques: every pairwise distance <= threshold) must be reduced again
+by the capacity-retry launch (betti_wide_kernel, big layout), never fail with DGN_ERR_CAPACITY.
+Counts and (birth, death) pairs bit-exact, compared as sorted multisets."""
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(low, n, thr):
+    return O.ref_persistence(low, n, thr) if O.ref_available() else O.persistence(low, n, thr)
+
+
+def _check(ctx, clouds, npts, thr, cap):
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=cap)
+    kt = ctx.kernel_times()
+    ctx.enable_timing(False)
+    bad = []
+    for c in range(len(npts)):
+        n = int(npts[c])
+        r = _ref(O.local_distances(clouds[c, :n]), n, np.float32(thr))
+        assert max(len(r[d]) for d in ("dim0", "dim1", "dim2")) <= cap, "raise the pair cap of this test"
+        got = {"dim0": pairs[c, 0, :counts[c, 0]], "dim1": pairs[c, 1, :counts[c, 2]], "dim2": pairs[c, 2, :counts[c, 3]]}
+        ok = all(np.array_equal(np.array(sorted(map(tuple, got[d]))).reshape(-1, 2), r[d].reshape(-1, 2))
+                 for d in got) and counts[c, 1] == r["n_inf0"]
+        if not ok:
+            bad.append((c, n, counts[c].tolist(), [len(r[d]) for d in ("dim0", "dim1", "dim2")], r["n_inf0"]))
+    assert not bad, bad[:8]
+    return kt
+
+
+def _cliques(rng, sizes, side=1.0):
+    maxp = max(sizes)
+    clouds = np.zeros((len(sizes), maxp, 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.uniform(0, side, size=(n, 3))
+    return clouds, np.array(sizes, dtype=np.int32)
+
+
+def test_clique_64_points(ctx):
+    """64 points, all pairwise distances <= threshold (the narrow kernel's largest tier)."""
+    rng = np.random.default_rng(31)
+    clouds, npts = _cliques(rng, [64, 64, 60, 48])
+    _check(ctx, clouds, npts, 2.0, 1 << 15)
+
+
+def test_clique_200_points(ctx):
+    """A 200-point clique: 1.3 M triangle columns (wide kernel, retried if its caps overflow)."""
+    rng = np.random.default_rng(37)
+    clouds, npts = _cliques(rng, [200])
+    kt = _check(ctx, clouds, npts, 2.0, 1 << 17)
+    print("retry launches:", kt.get("betti_retry", {}).get("launches", 0))
+
+
+def test_forced_capacity_retry_all_tiers(ctx, monkeypatch):
+    """Every complex of a batch spanning the three tiers (<= 48, 49..64, 65..) is routed through
+    the capacity-retry launch (DGN_FORCE_RETRY, a test knob) and still matches Ripser."""
+    rng = np.random.default_rng(41)
+    sizes = [5, 30, 48, 55, 64, 90, 130]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.uniform(0, 5.0, size=(n, 3))
+    monkeypatch.setenv("DGN_FORCE_RETRY", "1")
+    kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
+    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    monkeypatch.delenv("DGN_FORCE_RETRY")
+    kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
+    assert "betti_retry" not in kt
