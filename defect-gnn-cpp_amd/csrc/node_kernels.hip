@@ -100,7 +100,8 @@ __global__ __launch_bounds__(kEdgeRows) void edge_arrays_kernel(const int64_t* _
     const int64_t a0 = (int64_t)blockIdx.x * kEdgeRows;
     const int na = (int)(A - a0 < kEdgeRows ? A - a0 : kEdgeRows);
     const int t = threadIdx.x;
-    if (t <= na) rp_s[t] = row_ptr[a0 + t];
+    if (t < na) rp_s[t] = row_ptr[a0 + t];
+    if (t == 0) rp_s[na] = row_ptr[a0 + na];  // na <= kEdgeRows: one past the block's last row
     if (t < na && src) {
         // structure of atom a0 + t: the last s with atom_offset[s] <= a (binary search)
         const int64_t a = a0 + t;
