@@ -29,7 +29,6 @@
 namespace dgn {
 namespace {
 
-constexpr int kWW = kWideMaxPoints / 64;  // bitset words per vertex
 constexpr uint64_t kInfW = ~0ull;
 constexpr uint32_t kNoneW = 0xFFFFFFFFu;
 constexpr uint16_t kMcNoneW = 0xFFFF;     // not a column, or no cofacet
@@ -75,7 +74,10 @@ __device__ __forceinline__ uint64_t pinsert(int nv, uint64_t p, int x) {
 }
 __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 
+// KW: bitset words per vertex the instantiation handles (complexes of up to 64 KW points)
+template <int KW>
 struct WideCx {
+    static constexpr int kWW = KW;
     const BettiLaunch& bl;
     const WideLayout& ly;
     uint64_t* adj;  // LDS [n][W]: row v = the neighbours of vertex v, W words
@@ -211,7 +213,7 @@ struct WideCx {
     // a, b, c are returned for the apparent test.
     __device__ uint64_t min_cofacet(int dim, int a, int b, int c, uint32_t dsig, uint64_t sp_, const uint64_t* cand,
                                     uint64_t& bestp, int& bk, bool& found, uint32_t& hda, uint32_t& hdb,
-                                    uint32_t& hdc) const {
+                                    uint32_t& hdc, int* steps = nullptr) const {
         uint64_t best = kInfW;
         found = false;
         bk = 0;
@@ -237,6 +239,7 @@ struct WideCx {
                 if (val[j]) m &= ~(1ull << bit);
             }
             if (!val[0]) break;
+            if (steps) ++*steps;
             uint32_t da[4], dbv[4], dc[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -334,16 +337,32 @@ struct WideCx {
         return nna;
     }
 
-    // ---- dim 2: one lane per column (uncleared triangle), triangles streamed edge by edge ----
+    // ---- dim 2: one lane per column (uncleared triangle), a per-lane work queue ----
+    // Each lane owns an edge (a > b) of the edge list and the triangles (a, b, c), c < b, of its
+    // common neighbours; it walks one triangle's candidate cofacets four per step and takes its
+    // next triangle as soon as the walk ends (zero-persistence cofacet found, or candidates
+    // exhausted), so lanes never wait for the longest walk of a round (measured at 10 A: 2.1
+    // steps per column on average, 11 for the longest lane of a 64-column round). A fresh
+    // triangle's clearing mark and edge lengths are loaded together with its first candidates.
     __device__ int pass_dim2(int n_edges) {
+        [[maybe_unused]] const int lane = lane_id();
         const uint32_t* edges = sp<uint32_t>(ly.edges);
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
         int nna = 0, next_edge = 0;
-        int ea = 0, eb = 0, tw = -1;  // current edge (a > b) and word of c < b
-        uint64_t tm = 0;              // remaining c of the current word
+        int ea = 0, eb = 0, tw = -1;  // the lane's edge (a > b) and the word of its next c < b
+        uint64_t tm = 0;              // remaining c of that word
+        bool act = false, fresh = false;
+        int c = 0, w = 0, bk = 0;
+        uint64_t m = 0, tidx = 0, best = kInfW, bestp = 0;
+        uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, colp = 0, hda = 0, hdb = 0, hdc = 0;
+        bool found = false;
+#ifdef DGN_PHASE_TIMING
+        uint64_t nsteps = 0, niter = 0, ncols = 0;
+#endif
         for (;;) {
+            // (1) lanes without a triangle take the next c of their edge, or a new edge
             for (;;) {
-                while (tm == 0ull && tw >= 0) {  // next word of the current edge
+                while (!act && tm == 0ull && tw >= 0) {  // next word of the current edge
                     ++tw;
                     if (64 * tw >= eb) {
                         tw = -1;
@@ -353,7 +372,7 @@ struct WideCx {
                     const int lim = eb - 64 * tw;
                     if (lim < 64) tm &= (1ull << lim) - 1ull;
                 }
-                const bool need = tm == 0ull;
+                const bool need = !act && tm == 0ull;
                 const uint64_t bal = ballot(need);
                 if (!bal || next_edge >= n_edges) break;
                 const int e = next_edge + mask_prefix(bal);
@@ -367,40 +386,127 @@ struct WideCx {
                 }
                 next_edge += __popcll(bal);
             }
-            const bool active = tm != 0ull;
-            if (!ballot(active)) break;
-            bool na = false;
-            uint64_t colkey = 0, best = kInfW, bestp = 0;
-            uint32_t colp = 0;
-            if (active) {
-                const int a = ea, b = eb, c = 64 * tw + __ffsll((unsigned long long)tm) - 1;
+            if (!act && tm != 0ull) {
+                c = 64 * tw + __ffsll((unsigned long long)tm) - 1;
                 tm &= tm - 1ull;
-                const uint64_t tidx = bin3(a) + bin2(b) + c;
-                uint16_t mc = kMcNoneW;
-                if (mc_t[tidx] != kMcClearedW) {
-                    const uint32_t dab = d(a, b), dac = d(a, c), dbc = d(b, c);
-                    const uint32_t ds = max(max(dab, dac), dbc);
-                    colp = ((uint32_t)a << 18) | ((uint32_t)b << 9) | (uint32_t)c;
-                    colkey = wkey(ds, tidx);
-                    uint64_t cand[kWW];
+                act = fresh = true;
+                tidx = bin3(ea) + bin2(eb) + c;
+                colp = ((uint32_t)ea << 18) | ((uint32_t)eb << 9) | (uint32_t)c;
+                w = W - 1;
+                m = aw(ea, w) & aw(eb, w) & aw(c, w);
+                best = kInfW;
+                bestp = 0;
+                bk = 0;
+                found = false;
+            }
+            if (!ballot(act)) break;
+            bool na = false;
+            uint64_t colkey = 0, ntau = kInfW, ntv = 0;
+            uint32_t ncolp = 0;
+            if (act) {
+                const int a = ea, b = eb;
+                // (2) one step: up to four candidates, highest first
+                int kk[4];
+                bool val[4];
 #pragma unroll
-                    for (int w = 0; w < kWW; ++w) cand[w] = w < W ? (aw(a, w) & aw(b, w) & aw(c, w)) : 0ull;
-                    bool found;
-                    int bk;
-                    uint32_t hda = 0, hdb = 0, hdc = 0;
-                    best = min_cofacet(2, a, b, c, ds, colp, cand, bestp, bk, found, hda, hdb, hdc);
-                    if (best != kInfW) {
-                        const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
-                                         (bk > b || max(max(hda, hdc), dac) < ds) &&
-                                         (bk > c || max(max(hda, hdb), dab) < ds);
-                        na = !app;
-                        mc = (uint16_t)bk;
+                for (int j = 0; j < 4; ++j) {
+                    while (m == 0ull && w > 0) {
+                        --w;
+                        m = aw(a, w) & aw(b, w) & aw(c, w);
+                    }
+                    val[j] = m != 0ull;
+                    const int bit = val[j] ? 63 - __clzll((long long)m) : 0;
+                    kk[j] = 64 * w + bit;
+                    if (val[j]) m &= ~(1ull << bit);
+                }
+                uint32_t da[4], dbv[4], dc[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = val[j] ? kk[j] : c;
+                    da[j] = d(a, k);
+                    dbv[j] = d(b, k);
+                    dc[j] = d(c, k);
+                }
+                bool cleared = false;
+                if (fresh) {
+                    cleared = mc_t[tidx] == kMcClearedW;
+                    dab = d(a, b);
+                    dac = d(a, c);
+                    dbc = d(b, c);
+                    ds = max(max(dab, dac), dbc);
+                    fresh = false;
+                }
+#ifdef DGN_PHASE_TIMING
+                nsteps += 1;
+#endif
+                bool done;
+                if (cleared) {
+                    mc_t[tidx] = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
+                    done = true;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (!val[j] || found) continue;
+                        const int k = kk[j];
+                        const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
+                        const uint64_t p = pinsert(3, colp, k);
+                        const uint64_t idx = pidx(4, p);
+                        if (dk <= ds) {
+                            best = wkey(ds, idx);
+                            bestp = p;
+                            bk = k;
+                            found = true;
+                            hda = da[j];
+                            hdb = dbv[j];
+                            hdc = dc[j];
+                        } else {
+                            const uint64_t kk2 = wkey(dk, idx);
+                            if (kk2 < best) {
+                                best = kk2;
+                                bestp = p;
+                                bk = k;
+                            }
+                        }
+                    }
+                    done = found || !val[3];
+                    if (done) {
+                        // apparent iff (a, b, c) is the F-max facet of its zero-persistence cofacet
+                        uint16_t mc = kMcNoneW;
+                        if (best != kInfW) {
+                            const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
+                                             (bk > b || max(max(hda, hdc), dac) < ds) &&
+                                             (bk > c || max(max(hda, hdb), dab) < ds);
+                            na = !app;
+                            mc = (uint16_t)bk;
+                        }
+                        mc_t[tidx] = mc;
+                        colkey = wkey(ds, tidx);
+                        ntau = best;
+                        ntv = bestp;
+                        ncolp = colp;
+#ifdef DGN_PHASE_TIMING
+                        ncols += 1;
+#endif
                     }
                 }
-                mc_t[tidx] = mc;
+                if (done) act = false;
             }
-            na_append(na, nna, colkey, best, bestp, colp);
+            na_append(na, nna, colkey, ntau, ntv, ncolp);
+#ifdef DGN_PHASE_TIMING
+            niter += 1;
+#endif
         }
+#ifdef DGN_PHASE_TIMING
+        // walk steps: summed over lanes [26], wave iterations [27], columns walked [28]
+        if (bl.phase_cycles) {
+            const uint64_t tot = wave_sum(nsteps), cols = wave_sum(ncols);
+            if (lane == 0) {
+                atomicAdd(&bl.phase_cycles[26], (unsigned long long)tot);
+                atomicAdd(&bl.phase_cycles[27], (unsigned long long)niter);
+                atomicAdd(&bl.phase_cycles[28], (unsigned long long)cols);
+            }
+        }
+#endif
         __syncthreads();
         return nna;
     }
@@ -555,29 +661,36 @@ struct WideCx {
     __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
         const int k = lane_id();
         const uint32_t* VL = sp<uint32_t>(ly.vlist);
-        uint32_t* VD = sp<uint32_t>(ly.vdiam);
-        for (int i = k; i < v; i += kWave) VD[i] = sdiam(dim, VL[i]);
-        __syncthreads();
+        // V entries and their diameters live in registers (lane i: entry base + i), read back with
+        // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
+        const uint32_t vl0 = k < v ? VL[k] : 0u;
+        const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
         for (;;) {
             uint64_t lmin = kInfW, lp = 0;
             int lcnt = 0;
-            for (int i = 0; i < v; ++i) {
-                const uint32_t s = uniw(VL[i]);
-                const uint32_t ds = uniw(VD[i]);
+            auto eval = [&](uint32_t s, uint32_t ds) {
                 const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
                 const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
                 const int c = pv(s, 0);
-                for (int t = 0; t < W; ++t) {
-                    const int x = 64 * t + k;
+                // every word's row reads issued before any is used (coalesced rows a, b, c)
+                uint32_t da[KW], db[KW], dc[KW];
+#pragma unroll
+                for (int t = 0; t < KW; ++t) {
+                    const int x = min(64 * t + k, n - 1);
+                    da[t] = d(a, x);
+                    db[t] = d(b, x);
+                    dc[t] = dim == 2 ? d(c, x) : 0u;
+                }
+#pragma unroll
+                for (int t = 0; t < KW; ++t) {
+                    if (t >= W) break;
                     uint64_t am = aw(a, t) & aw(b, t);
                     if (dim == 2) am &= aw(c, t);
-                    const bool on = x < n && ((am >> k) & 1ull);
-                    const int xc = x < n ? x : n - 1;
-                    uint32_t dd = max(ds, max(d(a, xc), d(b, xc)));
-                    if (dim == 2) dd = max(dd, d(c, xc));
-                    const uint64_t p = pinsert(dim + 1, s, xc);
+                    const int x = 64 * t + k;
+                    const uint32_t dd = max(max(ds, dc[t]), max(da[t], db[t]));
+                    const uint64_t p = pinsert(dim + 1, s, x);
                     const uint64_t kk = wkey(dd, pidx(dim + 2, p));
-                    if (on && kk > floor) {
+                    if (((am >> k) & 1ull) && kk > floor) {  // x is a common neighbour (so x < n)
                         if (kk < lmin) {
                             lmin = kk;
                             lcnt = 1;
@@ -587,6 +700,20 @@ struct WideCx {
                         }
                     }
                 }
+            };
+            for (int base = 0; base < v; base += kWave) {
+                uint32_t vl = vl0, vd = vd0;
+                if (base > 0) {
+                    vl = base + k < v ? VL[base + k] : 0u;
+                    vd = base + k < v ? sdiam(dim, vl) : 0u;
+                }
+                const int cnt = v - base < kWave ? v - base : kWave;
+                int i = 0;
+                for (; i + 1 < cnt; i += 2) {  // two entries' distance reads in flight together
+                    eval(rlw(vl, i), rlw(vd, i));
+                    eval(rlw(vl, i + 1), rlw(vd, i + 1));
+                }
+                if (i < cnt) eval(rlw(vl, i), rlw(vd, i));
             }
             const uint64_t m = wave_min(lmin);
             if (m == kInfW) return kInfW;
@@ -821,6 +948,7 @@ struct WideCx {
     }
 };
 
+template <int KW>
 __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
     // [nmax] u16, the dequeue slot
@@ -846,12 +974,22 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
             continue;
         }
-        WideCx cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+        WideCx<KW> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
         cx.run(gi, bl.weight ? bl.weight[gi] : 1.0);
     }
 }
 
 int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
+
+// the instantiation for complexes of up to nmax points: 2, 4, 6 or 8 bitset words per vertex
+using WideKernel = void (*)(BettiLaunch, WideLayout);
+WideKernel wide_kernel_for(int nmax) {
+    const int w = (nmax + 63) / 64;
+    if (w <= 2) return betti_wide_kernel<2>;
+    if (w <= 4) return betti_wide_kernel<4>;
+    if (w <= 6) return betti_wide_kernel<6>;
+    return betti_wide_kernel<8>;
+}
 
 size_t wide_lds_bytes(int nmax) {
     const int64_t ww = (nmax + 63) / 64;
@@ -916,7 +1054,7 @@ int betti_wide_resident_waves(int device, int nmax) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_wide_kernel, kWave, wide_lds_bytes(nmax)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax), kWave, wide_lds_bytes(nmax)) !=
             hipSuccess ||
         per_cu <= 0)
         per_cu = 2;
@@ -925,7 +1063,7 @@ int betti_wide_resident_waves(int device, int nmax) {
 
 hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
     if (waves <= 0) return hipSuccess;
-    hipLaunchKernelGGL(betti_wide_kernel, dim3((unsigned)waves), dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
+    hipLaunchKernelGGL(wide_kernel_for(l.nmax), dim3((unsigned)waves), dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
     return hipGetLastError();
 }
 
