@@ -26,6 +26,10 @@
 
 #include "dgn_internal.hpp"
 
+#ifndef DGN_WIDE_STEP
+#define DGN_WIDE_STEP 4
+#endif
+
 namespace dgn {
 namespace {
 
@@ -338,6 +342,7 @@ struct WideCx {
     }
 
     // ---- dim 2: one lane per column (uncleared triangle), a per-lane work queue ----
+    static constexpr int kStep = DGN_WIDE_STEP;  // candidates per walk step (distance reads in flight)
     // Each lane owns an edge (a > b) of the edge list and the triangles (a, b, c), c < b, of its
     // common neighbours; it walks one triangle's candidate cofacets four per step and takes its
     // next triangle as soon as the walk ends (zero-persistence cofacet found, or candidates
@@ -405,11 +410,11 @@ struct WideCx {
             uint32_t ncolp = 0;
             if (act) {
                 const int a = ea, b = eb;
-                // (2) one step: up to four candidates, highest first
-                int kk[4];
-                bool val[4];
+                // (2) one step: up to kStep candidates, highest first
+                int kk[kStep];
+                bool val[kStep];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kStep; ++j) {
                     while (m == 0ull && w > 0) {
                         --w;
                         m = aw(a, w) & aw(b, w) & aw(c, w);
@@ -419,9 +424,9 @@ struct WideCx {
                     kk[j] = 64 * w + bit;
                     if (val[j]) m &= ~(1ull << bit);
                 }
-                uint32_t da[4], dbv[4], dc[4];
+                uint32_t da[kStep], dbv[kStep], dc[kStep];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < kStep; ++j) {
                     const int k = val[j] ? kk[j] : c;
                     da[j] = d(a, k);
                     dbv[j] = d(b, k);
@@ -445,7 +450,7 @@ struct WideCx {
                     done = true;
                 } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
+                    for (int j = 0; j < kStep; ++j) {
                         if (!val[j] || found) continue;
                         const int k = kk[j];
                         const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
@@ -468,7 +473,7 @@ struct WideCx {
                             }
                         }
                     }
-                    done = found || !val[3];
+                    done = found || !val[kStep - 1];
                     if (done) {
                         // apparent iff (a, b, c) is the F-max facet of its zero-persistence cofacet
                         uint16_t mc = kMcNoneW;
