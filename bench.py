@@ -17,6 +17,9 @@ Rank 0 prints ONE JSON line (metric/unit from BASELINE.json) with
   roofline      the neighbour + RBF path (prep + count + scan + emit, HBM-bound) at SURVEY 8(d)'s
                 algorithmic bytes over its HIP-event time on the launch stream; the emit launch
                 alone and the f64-RBF variant (measured after the timed loop) beside it
+  side          beside the headline, never part of `value`: BASELINE configs 2, 3 and 5 (1,024 x
+                SC-64 graph / graph + Betti, one 4,096-atom supercell) and the Betti pass at the
+                reference's default 10 A cutoff (32 FCC-256 structures, wide kernel)
   cpu_baseline  the reference CPU path on this host on a bounded sample of the same shard
                 (restated neighbour list + the reference's verbatim vendored Ripser), at the
                 reference's default nesting and at OMP x 1 Ripser thread; its outputs double as the
@@ -53,6 +56,9 @@ def parse():
     ap.add_argument("--betti-rc", type=float, default=5.0)
     ap.add_argument("--no-betti", action="store_true", help="graph only (config 2 style)")
     ap.add_argument("--no-f64", action="store_true", help="skip the f64-RBF side measurement")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the side lines (BASELINE configs 2/3/5 and the 10 A Betti line)")
+    ap.add_argument("--side-reps", type=int, default=3)
     ap.add_argument("--cpu-sample", type=int, default=64, help="structures in each CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -193,6 +199,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(args, sh, n_atoms, torch)
+    if not args.no_side and world == 1:
+        result["side"] = side_lines(dgn, abi, ctx, dev, args, torch)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -222,6 +230,65 @@ def f64_side_measurement(ctx, sh, args, nbins, abi, dgn, torch):
     return {"algorithmic_bytes_per_launch": int(algo), "avg_launch_ms": round(path_ms, 4),
             "achieved": round(algo / (path_ms * 1e-3) / 1e9, 1),
             "frac": round(algo / (path_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "emit_ms": round(emit_ms, 4)}
+
+
+def side_lines(dgn, abi, ctx, dev, args, torch):
+    """Beside the headline (never part of `value`): the other BASELINE configs on one GPU and the
+    Betti pass at the reference's default 10 A cutoff (preprocess_betti.cpp:117). Each: the
+    whole path through the C ABI, inputs resident, `reps` timed repetitions after one warm-up."""
+    from dgn.shard import Shard
+    out = {}
+
+    def timed(sh, gp, betti_rc, betti, graph=True):
+        sh.step(ctx, gp, betti_rc, betti=betti, graph=graph)
+        torch.cuda.synchronize(dev)
+        ctx.reset_timing()
+        ctx.enable_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(args.side_reps):
+            sh.step(ctx, gp, betti_rc, betti=betti, graph=graph)
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / args.side_reps
+        kt = ctx.kernel_times()
+        ctx.enable_timing(False)
+        return dt, {k: round(v["total_ms"] / args.side_reps, 4) for k, v in kt.items()}
+
+    gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F32)
+    nb = abi.lib().dgn_rbf_bins(5.0, 0.1)
+    # configs 2 and 3: 1,024 jittered SC-64 cells, graph only / graph + Betti (rc 5)
+    sh = Shard(dgn, abi, "sc", 4, 1024, 0, dev)
+    sh.alloc_graph(ctx, gp, nb, torch.float32)
+    sh.alloc_betti()
+    dt, kt = timed(sh, gp, 5.0, False)
+    gk = sum(kt.get(k, 0.0) for k in GRAPH_KERNELS)
+    algo = graph_bytes_8d(sh.A, sh.B, sh.E, nb, 4)
+    out["config2"] = {"workload": "1024 x SC-64, NeighborList(5, 20) + 50-bin f32 RBF", "structures_per_s": round(sh.B / dt, 1),
+                      "ms": round(dt * 1e3, 4), "path_ms": round(gk, 4),
+                      "path_hbm_frac": round(algo / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if gk else None}
+    dt, kt = timed(sh, gp, 5.0, True)
+    out["config3"] = {"workload": "1024 x SC-64, graph + Betti-0/1/2 (rc 5)", "structures_per_s": round(sh.B / dt, 1),
+                      "ms": round(dt * 1e3, 4), "betti_vr_ms": kt.get("betti_vr")}
+    del sh
+    # config 5: one 4,096-atom SC supercell (27 images), graph + Betti
+    sh = Shard(dgn, abi, "sc", 16, 1, 0, dev)
+    sh.alloc_graph(ctx, gp, nb, torch.float32)
+    sh.alloc_betti()
+    dt, kt = timed(sh, gp, 5.0, False)
+    gk = sum(kt.get(k, 0.0) for k in GRAPH_KERNELS)
+    dt2, kt2 = timed(sh, gp, 5.0, True, graph=False)
+    out["config5"] = {"workload": "1 x SC-4096 supercell (L = 37.1 A), graph rc 5 K 20 + Betti rc 5",
+                      "graph_ms": round(dt * 1e3, 4), "graph_path_kernels_ms": round(gk, 4),
+                      "graph_path_hbm_frac": round(graph_bytes_8d(sh.A, 1, sh.E, nb, 4) / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                      if gk else None, "betti_ms": round(dt2 * 1e3, 4)}
+    del sh
+    # the reference's default Betti cutoff, 10 A (~340-point complexes, wide kernel)
+    sh = Shard(dgn, abi, "fcc", 4, 32, 0, dev)
+    sh.alloc_betti()
+    dt, kt = timed(sh, gp, 10.0, True, graph=False)
+    out["betti_rc10"] = {"workload": "32 x FCC-256 (8,192 complexes of ~340 points), Betti-0/1/2 at rc 10",
+                         "structures_per_s": round(sh.B / dt, 2), "complexes_per_s": round(sh.A / dt, 1),
+                         "ms": round(dt * 1e3, 2), "betti_vr_ms": kt.get("betti_vr")}
+    return out
 
 
 def cpu_model():
