@@ -48,9 +48,6 @@ constexpr uint32_t kECapacity = kEWork | kENA | kEPiv | kEPairs | kER | kEGuard;
 __device__ __forceinline__ uint64_t bin2(uint64_t v) { return v * (v - 1) / 2; }
 __device__ __forceinline__ uint64_t bin3(uint64_t v) { return v * (v - 1) * (v - 2) / 6; }
 __device__ __forceinline__ uint64_t bin4(uint64_t v) { return v * (v - 1) * (v - 2) * (v - 3) / 24; }
-__device__ __forceinline__ uint64_t wkey(uint32_t dbits, uint64_t idx) {
-    return ((uint64_t)dbits << 32) | (uint64_t)(~(uint32_t)idx);
-}
 __device__ __forceinline__ uint32_t rlw(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
 __device__ __forceinline__ uint64_t rlw64(uint64_t x, int l) {
     return ((uint64_t)rlw((uint32_t)(x >> 32), l) << 32) | rlw((uint32_t)x, l);
@@ -61,27 +58,38 @@ __device__ __forceinline__ uint64_t uniw64(uint64_t x) {
 }
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
-// packed simplex: vertices 9 bits each, descending, the smallest in the low field
-__device__ __forceinline__ int pv(uint64_t p, int field) { return (int)((p >> (9 * field)) & 511); }
 // combinatorial index of a packed simplex with nv vertices
-__device__ __forceinline__ uint64_t pidx(int nv, uint64_t p) {
-    if (nv == 2) return bin2(pv(p, 1)) + pv(p, 0);
-    if (nv == 3) return bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
-    return bin4(pv(p, 3)) + bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
-}
 // insert vertex x (not in p) into a packed simplex of nv vertices
-__device__ __forceinline__ uint64_t pinsert(int nv, uint64_t p, int x) {
-    int below = 0;
-    for (int t = 0; t < nv; ++t) below += pv(p, t) < x;
-    const uint64_t mask = (1ull << (9 * below)) - 1;
-    return ((p & ~mask) << 9) | ((uint64_t)x << (9 * below)) | (p & mask);
-}
 __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 
-// KW: bitset words per vertex the instantiation handles (complexes of up to 64 KW points)
-template <int KW>
+// KW: bitset words per vertex the instantiation handles (complexes of up to 64 KW points).
+// BIG (complexes of 513..1024 points): vertices packed in 10 bits, distances replaced by their
+// rank codes in the complex (order- and equality-preserving, < 2^20; betti_rank_codes) so a
+// simplex key (code << 36) | ~index fits 64 bits (C(1024, 4) < 2^36); code -> f32 via the
+// complex's sorted distances. Otherwise 9-bit vertices and (f32 bits << 32) | ~index keys.
+template <int KW, bool BIG>
 struct WideCx {
     static constexpr int kWW = KW;
+    static constexpr int VB = BIG ? 10 : 9;            // bits per packed vertex
+    static constexpr uint64_t VM = (1ull << VB) - 1;
+    static constexpr int KS = BIG ? 36 : 32;           // key: (distance code << KS) | ~index
+    __device__ static int pv(uint64_t p, int field) { return (int)((p >> (VB * field)) & VM); }
+    __device__ static uint64_t pidx(int nv, uint64_t p) {
+        if (nv == 2) return bin2(pv(p, 1)) + pv(p, 0);
+        if (nv == 3) return bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
+        return bin4(pv(p, 3)) + bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
+    }
+    __device__ static uint64_t pinsert(int nv, uint64_t p, int x) {
+        int below = 0;
+        for (int t = 0; t < nv; ++t) below += pv(p, t) < x;
+        const uint64_t mask = (1ull << (VB * below)) - 1;
+        return ((p & ~mask) << VB) | ((uint64_t)x << (VB * below)) | (p & mask);
+    }
+    __device__ static uint64_t wkey(uint32_t dc, uint64_t idx) {
+        return ((uint64_t)dc << KS) | (~idx & ((1ull << KS) - 1));
+    }
+    __device__ static uint32_t kdiam(uint64_t key) { return (uint32_t)(key >> KS); }
+    __device__ static uint32_t pack_edge(int i, int j) { return ((uint32_t)i << VB) | (uint32_t)j; }
     const BettiLaunch& bl;
     const WideLayout& ly;
     uint64_t* adj;  // LDS [n][W]: row v = the neighbours of vertex v, W words
@@ -91,6 +99,9 @@ struct WideCx {
     float thr;
     uint32_t err;
     int n_d0, n_inf0, n_p1, n_p2;
+    const uint32_t* vals = nullptr;  // BIG: the complex's sorted f32 distances (code -> value)
+
+    __device__ float value(uint32_t dc) const { return BIG ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
 
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
@@ -103,12 +114,13 @@ struct WideCx {
     }
 
     // ---- distance matrix (mirrored from the packed lower triangle) + adjacency bitsets ----
-    __device__ void load(int64_t gi) {
+    __device__ void load(int64_t gi, int64_t slot) {
         const int lane = lane_id();
         const float* L = bl.lower + gi * bl.tri_stride;
-        float* D = sp<float>(ly.D);
+        uint32_t* D = sp<uint32_t>(ly.D);
+        const uint32_t* Lc = BIG ? bl.rank_codes + slot * bl.rank_stride : nullptr;
         for (int i = lane; i < n * W; i += kWave) adj[i] = 0ull;
-        for (int i = lane; i < n; i += kWave) D[(int64_t)i * n + i] = 0.0f;
+        for (int i = lane; i < n; i += kWave) D[(int64_t)i * n + i] = 0u;  // 0.0f, or code 0 (BIG: unused)
         wave_lds_order();
         for (int i = 1; i < n; ++i) {
             for (int j0 = 0; j0 < i; j0 += kWave) {
@@ -116,8 +128,9 @@ struct WideCx {
                 bool e = false;
                 if (j < i) {
                     const float v = L[c2i(i) + j];
-                    D[(int64_t)i * n + j] = v;
-                    D[(int64_t)j * n + i] = v;
+                    const uint32_t dv = BIG ? Lc[c2i(i) + j] : __float_as_uint(v);
+                    D[(int64_t)i * n + j] = dv;
+                    D[(int64_t)j * n + i] = dv;
                     e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
                 }
                 const uint64_t b = ballot(e);
@@ -169,9 +182,9 @@ struct WideCx {
                 const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
                 v = 64 * (int)rlw((uint32_t)lt, l) + l;
                 const int u = (int)rlw((uint32_t)lp, l);
-                const uint32_t dd = (uint32_t)(m >> 32);
-                if (dd != 0u) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
-                    if (lane == 0) d0s[n_d0] = __uint_as_float(dd);
+                const uint32_t dd = kdiam(m);
+                if (value(dd) != 0.0f) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
+                    if (lane == 0) d0s[n_d0] = value(dd);
                     ++n_d0;
                 }
                 if (lane == 0) par[v] = (uint16_t)u;
@@ -203,7 +216,7 @@ struct WideCx {
                 uint64_t bits = aw(i, w);
                 const int lim = i - 64 * w;
                 if (lim < 64) bits &= (1ull << lim) - 1ull;
-                if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = ((uint32_t)i << 9) | (uint32_t)(64 * w + lane);
+                if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = pack_edge(i, 64 * w + lane);
                 off += __popcll(bits);
             }
         __syncthreads();
@@ -310,7 +323,7 @@ struct WideCx {
             uint32_t colp = 0;
             if (e < n_edges) {
                 const uint32_t ed = edges[e];
-                const int i = (int)(ed >> 9), j = (int)(ed & 511);
+                const int i = (int)(ed >> VB), j = (int)(ed & VM);
                 uint16_t mc = kMcNoneW;
                 if (!is_tree(i, j)) {
                     const uint32_t dij = d(i, j);
@@ -383,8 +396,8 @@ struct WideCx {
                 const int e = next_edge + mask_prefix(bal);
                 if (need && e < n_edges) {
                     const uint32_t ed = edges[e];
-                    ea = (int)(ed >> 9);
-                    eb = (int)(ed & 511);
+                    ea = (int)(ed >> VB);
+                    eb = (int)(ed & VM);
                     tw = 0;
                     tm = aw(ea, 0) & aw(eb, 0);
                     if (eb < 64) tm &= (1ull << eb) - 1ull;
@@ -396,7 +409,7 @@ struct WideCx {
                 tm &= tm - 1ull;
                 act = fresh = true;
                 tidx = bin3(ea) + bin2(eb) + c;
-                colp = ((uint32_t)ea << 18) | ((uint32_t)eb << 9) | (uint32_t)c;
+                colp = ((uint32_t)ea << (2 * VB)) | ((uint32_t)eb << VB) | (uint32_t)c;
                 w = W - 1;
                 m = aw(ea, w) & aw(eb, w) & aw(c, w);
                 best = kInfW;
@@ -615,7 +628,7 @@ struct WideCx {
             uint64_t f = 0;
             for (int s = 0; s < nv; ++s) {
                 if (s == t) continue;
-                f = (f << 9) | (uint64_t)v[s];
+                f = (f << VB) | (uint64_t)v[s];
                 for (int u = s + 1; u < nv; ++u)
                     if (u != t) diam = max(diam, dd[s][u]);
             }
@@ -775,7 +788,7 @@ struct WideCx {
             uint64_t tau = uniw64(T[ci]);
             uint64_t tv = uniw64(V[ci]);
             const uint32_t cp = uniw(Cc[ci]);
-            const uint32_t birth = (uint32_t)(colkey >> 32);
+            const uint32_t birth = kdiam(colkey);
             uint64_t meta = hfind(tau);
             WSUB(1);
             uint32_t app = meta == kNoMetaW ? apparent_owner(dim, tv) : kNoneW;
@@ -821,9 +834,9 @@ struct WideCx {
                 }
                 if (err || tau == kInfW) continue;
             }
-            const uint32_t death = (uint32_t)(tau >> 32);
-            if (__uint_as_float(death) > __uint_as_float(birth)) {
-                if (lane == 0 && np < ly.p_cap) pairs[np] = make_float2(__uint_as_float(birth), __uint_as_float(death));
+            const uint32_t death = kdiam(tau);
+            if (value(death) > value(birth)) {
+                if (lane == 0 && np < ly.p_cap) pairs[np] = make_float2(value(birth), value(death));
                 ++np;
             }
             if (dim == 1 && lane == 0) sp<uint16_t>(ly.mc_t)[pidx(3, tv)] = kMcClearedW;  // clearing
@@ -902,7 +915,7 @@ struct WideCx {
         }
     }
 
-    __device__ void run(int64_t gi, double weight) {
+    __device__ void run(int64_t gi, int64_t slot, double weight) {
 #ifdef DGN_PHASE_TIMING
         // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
         uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -917,7 +930,7 @@ struct WideCx {
     do {          \
     } while (0)
 #endif
-        load(gi);
+        load(gi, slot);
         WSTAMP(0);
         prim();
         const int n_edges = edge_list();
@@ -953,7 +966,7 @@ struct WideCx {
     }
 };
 
-template <int KW>
+template <int KW, bool BIG>
 __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
     // [nmax] u16, the dequeue slot
@@ -973,14 +986,20 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
         if (wi >= total) break;
         const int64_t gi = (int64_t)bl.wide_list[wi];
         const int n = bl.npoints[gi];
+        if (n > ly.nmax && bl.retry_list) {
+            // above this launch's envelope (512 points): the retry launch's BIG instantiation
+            if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+            continue;
+        }
         if (n > ly.nmax) {
             if (lane == 0) atomicOr(bl.error_flag, kEPoints);
             if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
             continue;
         }
-        WideCx<KW> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
-        cx.run(gi, bl.weight ? bl.weight[gi] : 1.0);
+        WideCx<KW, BIG> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+        if (BIG) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+        cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
     }
 }
 
@@ -990,10 +1009,11 @@ int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 using WideKernel = void (*)(BettiLaunch, WideLayout);
 WideKernel wide_kernel_for(int nmax) {
     const int w = (nmax + 63) / 64;
-    if (w <= 2) return betti_wide_kernel<2>;
-    if (w <= 4) return betti_wide_kernel<4>;
-    if (w <= 6) return betti_wide_kernel<6>;
-    return betti_wide_kernel<8>;
+    if (w <= 2) return betti_wide_kernel<2, false>;
+    if (w <= 4) return betti_wide_kernel<4, false>;
+    if (w <= 6) return betti_wide_kernel<6, false>;
+    if (w <= 8) return betti_wide_kernel<8, false>;
+    return betti_wide_kernel<16, true>;  // 513..1024 points: rank-coded distances (BIG)
 }
 
 size_t wide_lds_bytes(int nmax) {
@@ -1011,7 +1031,7 @@ WideLayout betti_wide_layout(int nmax, bool big) {
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
     int64_t cap = 1024;
-    const int64_t cap_max = big ? (int64_t(1) << 30) : (int64_t(1) << 17);
+    const int64_t cap_max = big ? (int64_t(1) << 24) : (int64_t(1) << 17);
     while ((cap < t || cap < e) && cap < cap_max) cap <<= 1;
     l.nmax = nmax;
     l.na_cap = (int32_t)cap;

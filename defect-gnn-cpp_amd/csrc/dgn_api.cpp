@@ -112,7 +112,7 @@ struct dgn_ctx {
     HostScalars* host = nullptr;  // pinned
     bool emit_pending = false;    // an emit's error flag is on its way to host->emit_flag
     // betti workspace
-    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big;
+    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big, b_rank, b_rscal;
     int betti_slots = 0;
     bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
@@ -393,14 +393,15 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     WideLayout wl{};
     int wide_waves = 0;
     if (max_points > 64) {
-        wl = betti_wide_layout(max_points);
+        const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
+        wl = betti_wide_layout(wide_nmax);
         // as many waves as the device keeps resident (dynamic LDS sized by max_points), each
         // with its own scratch, within half of the free HBM (288 GB per MI355X; at least 8 GB)
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
-        const int64_t resident = betti_wide_resident_waves(c->device, max_points);
+        const int64_t resident = betti_wide_resident_waves(c->device, wide_nmax);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         if (const char* ev = std::getenv("DGN_WIDE_WAVES")) {  // A/B experiments only
             const int w = std::atoi(ev);
@@ -410,12 +411,12 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
-        if (grown || c->wide_nmax != max_points || c->wide_waves != wide_waves) {
+        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves) {
             // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
             // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
             // restores both for the entries it used
             HIP_TRY(c, betti_wide_init_scratch(c->stream, wl, wide_waves));
-            c->wide_nmax = max_points;
+            c->wide_nmax = wide_nmax;
             c->wide_waves = wide_waves;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
@@ -474,31 +475,63 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         const int64_t nretry = c->host->s.retry_len;
         if (nretry == 0) return DGN_OK;
+        // complexes above kWideRegular points (listed by the regular wide launch) run on rank codes
+        // (betti_rank_codes, the BIG instantiation), in slices of at most 512 complexes
         const int nmax = std::max(max_points, 64);
+        const bool coded = nmax > kWideRegular;
         WideLayout big = betti_wide_layout(nmax, true);
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-        const int64_t budget = (int64_t)(free_b / 2) + (int64_t)c->b_big.bytes;
-        const int64_t waves = std::min<int64_t>({nretry, budget / big.total, betti_wide_resident_waves(c->device, nmax)});
+        const int64_t rstride = ((int64_t)nmax * (nmax - 1) / 2 + 63) / 64 * 64;
+        const int64_t slice = coded ? std::min<int64_t>(nretry, 512) : nretry;
+        const size_t rank_bytes = coded ? betti_rank_temp_bytes(slice, rstride) + 8 * (size_t)slice * rstride : 0;
+        const int64_t budget = (int64_t)(free_b / 2) + (int64_t)c->b_big.bytes - (int64_t)rank_bytes;
+        const int64_t waves =
+            std::min<int64_t>({slice, budget / big.total, betti_wide_resident_waves(c->device, nmax)});
         if (waves < 1)
             return fail(c, DGN_ERR_CAPACITY, "capacity retry: no device memory for a " + std::to_string(big.total) +
                                                  "-byte workspace");
         HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
         big.base = c->b_big.as<uint8_t>();
         HIP_TRY(c, betti_wide_init_scratch(c->stream, big, (int)waves));
+        if (coded) {
+            HIP_TRY(c, c->b_rank.ensure(rank_bytes));
+            HIP_TRY(c, c->b_rscal.ensure(sizeof(uint32_t) * 2 * (size_t)((nretry + slice - 1) / slice)));
+        }
         BettiLaunch rb = pb;
-        rb.wide_list = c->b_rlist.as<int32_t>();
-        rb.wide_len = &sc->retry_len;
-        rb.wide_queue = &sc->retry_queue;
         rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
         rb.retry_len = nullptr;
         rb.force_retry = 0;
-        {
+        std::vector<uint32_t> lens;
+        for (int64_t r0 = 0; r0 < nretry; r0 += slice) {
+            const int64_t cnt = std::min<int64_t>(slice, nretry - r0);
+            rb.wide_list = c->b_rlist.as<int32_t>() + r0;
+            if (coded) {
+                uint32_t* codes = c->b_rank.as<uint32_t>();
+                uint32_t* sorted = codes + slice * rstride;
+                void* tmp = sorted + slice * rstride;
+                HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, rb.wide_list, cnt, rstride,
+                                            codes, sorted, tmp, rank_bytes - 8 * (size_t)slice * rstride));
+                rb.rank_codes = codes;
+                rb.rank_sorted = sorted;
+                rb.rank_stride = rstride;
+                uint32_t* sl = c->b_rscal.as<uint32_t>() + 2 * (r0 / slice);
+                lens.push_back((uint32_t)cnt);
+                HIP_TRY(c, hipMemsetAsync(sl, 0, 2 * sizeof(uint32_t), c->stream));
+                HIP_TRY(c, hipMemcpyAsync(sl, &lens.back(), sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` may reallocate
+                rb.wide_len = sl;
+                rb.wide_queue = sl + 1;
+            } else {
+                rb.wide_len = &sc->retry_len;
+                rb.wide_queue = &sc->retry_queue;
+            }
             TimedLaunch t(c, "betti_retry", 0.0, 0.0);
-            HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)waves));
+            HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)std::min<int64_t>(waves, cnt)));
         }
         // the regular wide layout's tables are not touched; the big buffer is kept for reuse
         HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
         return DGN_OK;
     };
     // triangles: floats per complex, padded to a multiple of 4 (16-byte aligned complexes)

@@ -113,9 +113,17 @@ struct BettiLaunch {
     int32_t* retry_list;      // [num_atoms]
     uint32_t* retry_len;
     int32_t force_retry;      // tests (DGN_FORCE_RETRY=1): every narrow/wide complex takes the retry path
+    // complexes above kWideRegular points (the retry launch's BIG wide instantiation): per retry
+    // slot r, rank codes of the packed lower triangle and the sorted f32 distances (betti_rank_codes)
+    const uint32_t* rank_codes;  // [slots][rank_stride]
+    const uint32_t* rank_sorted; // [slots][rank_stride]
+    int64_t rank_stride;
 };
-// wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout
-constexpr int kWideMaxPoints = 512;
+// wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout. Up to
+// kWideRegular points in the regular launch; above it (rank-coded, 10-bit vertices) in the retry
+// launch after betti_rank_codes
+constexpr int kWideMaxPoints = 1024;
+constexpr int kWideRegular = 512;
 struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
@@ -126,6 +134,14 @@ struct WideLayout {
 WideLayout betti_wide_layout(int nmax, bool big = false);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax);  // device-wide resident waves (occupancy API)
+// rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
+// occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
+// equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,
+// size from betti_rank_temp_bytes.
+size_t betti_rank_temp_bytes(int64_t count, int64_t stride);
+hipError_t betti_rank_codes(hipStream_t s, const float* lower, int64_t tri_stride, const int32_t* npoints,
+                            const int32_t* list, int64_t count, int64_t stride, uint32_t* codes, uint32_t* sorted,
+                            void* temp, size_t temp_bytes);
 
 // distance pass over complexes [first, first + count) of a BettiLaunch's cloud input
 struct DistLaunch {

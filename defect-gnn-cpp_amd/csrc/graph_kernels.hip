@@ -1532,6 +1532,9 @@ hipError_t launch_betti_dist_search(hipStream_t s, const GraphLaunch& g, int64_t
     if (max_points <= kWave)
         hipLaunchKernelGGL(betti_dist_search_kernel<kWave>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, first,
                            count, tri_stride, counts, lower, npoints, error_flag, keys_out, key_stride);
+    else if (max_points <= kWideRegular)
+        hipLaunchKernelGGL(betti_dist_search_kernel<kWideRegular>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g,
+                           first, count, tri_stride, counts, lower, npoints, error_flag, keys_out, key_stride);
     else
         hipLaunchKernelGGL(betti_dist_search_kernel<kWideMaxPoints>, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g,
                            first, count, tri_stride, counts, lower, npoints, error_flag, keys_out, key_stride);
