@@ -1145,8 +1145,17 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int n = gi < bl.num_atoms ? bl.npoints[gi] : 0;
     const bool mid = gi < bl.num_atoms && n > np_small && n <= 64;
-    const bool wide = gi < bl.num_atoms && n > 64;
-    const uint64_t bm = ballot(mid), bw = ballot(wide);
+    // above kWideRegular points: straight to the retry list (rank-coded BIG launch)
+    const bool huge = gi < bl.num_atoms && n > kWideRegular && bl.retry_list;
+    const bool wide = gi < bl.num_atoms && n > 64 && !huge;
+    const uint64_t bm = ballot(mid), bw = ballot(wide), bh = ballot(huge);
+    if (bh) {
+        const int leader = __ffsll((unsigned long long)bh) - 1;
+        uint32_t base = 0;
+        if (lane_id() == leader) base = atomicAdd(bl.retry_len, (uint32_t)__popcll(bh));
+        base = (uint32_t)__shfl((int)base, leader, kWave);
+        if (huge) bl.retry_list[base + mask_prefix(bh)] = (int32_t)gi;
+    }
     if (bm) {
         const int leader = __ffsll((unsigned long long)bm) - 1;
         uint32_t base = 0;

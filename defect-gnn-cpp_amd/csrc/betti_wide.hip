@@ -986,20 +986,19 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
         if (wi >= total) break;
         const int64_t gi = (int64_t)bl.wide_list[wi];
         const int n = bl.npoints[gi];
-        if (n > ly.nmax && bl.retry_list) {
-            // above this launch's envelope (512 points): the retry launch's BIG instantiation
-            if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
-            continue;
-        }
+        // (no `continue` out of this loop: on gfx950 a uniform continue right after a lane-0
+        // atomic was seen to hang the wave; the branches rejoin instead)
+        // complexes above kWideRegular points never reach the regular launch (the bucket pass lists
+        // them for the rank-coded retry launch); a larger one here is outside the layout
         if (n > ly.nmax) {
             if (lane == 0) atomicOr(bl.error_flag, kEPoints);
             if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
-            continue;
+        } else {
+            WideCx<KW, BIG> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+            if (BIG) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+            cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
         }
-        WideCx<KW, BIG> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
-        if (BIG) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
-        cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
     }
 }
 

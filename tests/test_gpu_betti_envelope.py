@@ -7,6 +7,7 @@ Counts and (birth, death) pairs bit-exact, compared as sorted multisets."""
 import numpy as np
 import pytest
 
+import dgn
 import oracle_py as O
 
 pytestmark = pytest.mark.gpu
@@ -88,3 +89,18 @@ def test_cloud_above_512_points(ctx):
     clouds[1, 10] = clouds[1, 3]  # a duplicate point: zero distance, dim-0 pair not emitted
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.6, 1 << 14)
     assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
+def test_fcc256_cutoff_12A_above_512_points(ctx):
+    """compute_structure_betti_features at r_cutoff = 12: FCC-256 local complexes of ~580 points
+    (neighbour search at K = inf with up to 1,024 candidates, the rank-coded retry launch); one
+    atom spot-checked against the verbatim Ripser."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    f, c = ctx.host_betti(batch, 12.0)
+    assert not np.isnan(f).any()
+    assert c[:, 0].max() + 1 > 512  # complexes above the regular wide envelope
+    atoms = [5]
+    fo, co = O.ref_atom_betti(batch["lattice"][0], batch["positions"], batch["species"], 12.0, atoms)
+    assert np.array_equal(c[atoms], co), (c[atoms], co)
+    np.testing.assert_allclose(f[atoms], fo, rtol=1e-6, atol=1e-12)
