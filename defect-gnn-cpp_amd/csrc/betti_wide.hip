@@ -643,6 +643,80 @@ struct WideCx {
         return uniw(m) == (uint32_t)v[drop] ? (uint32_t)bestf : kNoneW;
     }
 
+    // Owner of the pivot tau in one round trip where possible: the first 64-slot window of the
+    // pivot table (keys and metadata) and tau's edge lengths (lane p loads edge p) are loaded
+    // together; a table hit returns its metadata (app = kNone), otherwise the apparent owner is
+    // decided from the edge lengths already in registers and one min-cofacet table read
+    // (apparent_owner's logic). Returns kNoMetaW when tau is not in the table.
+    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, uint32_t& app) const {
+        const int lane = lane_id();
+        const uint64_t* HK = sp<uint64_t>(ly.h_key);
+        const uint64_t* HM = sp<uint64_t>(ly.h_meta);
+        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
+        const uint32_t slot = (hmix(tau) + (uint32_t)lane) & mask;
+        const uint64_t hk = HK[slot];
+        const uint64_t hm = HM[slot];
+        const int nv = dim + 2;
+        const int v0 = pv(tv, nv - 1), v1 = pv(tv, nv - 2), v2 = pv(tv, nv - 3), v3 = nv == 4 ? pv(tv, 0) : 0;
+        // edge p of tau (vertices descending v0 > v1 > ...): (s, t) from nibble tables
+        const int np = nv == 4 ? 6 : 3;
+        const int lp = lane < np ? lane : 0;
+        const int ps = (int)(((nv == 4 ? 0x211000u : 0x100u) >> (4 * lp)) & 0xFu);
+        const int pt = (int)(((nv == 4 ? 0x332321u : 0x221u) >> (4 * lp)) & 0xFu);
+        const int va = ps == 0 ? v0 : (ps == 1 ? v1 : v2);
+        const int vb = pt == 1 ? v1 : (pt == 2 ? v2 : v3);
+        const uint32_t dl = d(va, vb);
+        const uint64_t hit = ballot(hk == tau), emp = ballot(hk == 0ull);
+        const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
+        const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
+        app = kNoneW;
+        if (fh < fe) return rlw64(hm, fh);
+        if (fe == kWave) {  // the window was full: probe on (rare at load factor <= 1/2)
+            const uint64_t m = hfind(tau);
+            if (m != kNoMetaW) return m;
+        }
+        uint32_t dd[4][4];
+        if (nv == 4) {
+            dd[0][1] = rlw(dl, 0);
+            dd[0][2] = rlw(dl, 1);
+            dd[0][3] = rlw(dl, 2);
+            dd[1][2] = rlw(dl, 3);
+            dd[1][3] = rlw(dl, 4);
+            dd[2][3] = rlw(dl, 5);
+        } else {
+            dd[0][1] = rlw(dl, 0);
+            dd[0][2] = rlw(dl, 1);
+            dd[1][2] = rlw(dl, 2);
+        }
+        const int v[4] = {v0, v1, v2, v3};
+        uint64_t bestk = 0, bestf = 0;
+        int drop = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {  // facet without v[t]
+            if (t >= nv) break;
+            uint32_t diam = 0;
+            uint64_t f = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                if (s2 >= nv || s2 == t) continue;
+                f = (f << VB) | (uint64_t)v[s2];
+#pragma unroll
+                for (int u = s2 + 1; u < 4; ++u)
+                    if (u < nv && u != t) diam = max(diam, dd[s2][u]);
+            }
+            const uint64_t kk = wkey(diam, pidx(nv - 1, f));
+            if (kk > bestk) {
+                bestk = kk;
+                bestf = f;
+                drop = t;
+            }
+        }
+        const uint16_t m = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
+        const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
+        if (uniw(m) == (uint32_t)vd) app = (uint32_t)bestf;
+        return kNoMetaW;
+    }
+
     // ---- the working column's V list (scratch: vlist[0..v), packed simplices, no small cap) ----
     __device__ int v_find(uint32_t x, int v) const {
         const int lane = lane_id();
@@ -789,10 +863,9 @@ struct WideCx {
             uint64_t tv = uniw64(V[ci]);
             const uint32_t cp = uniw(Cc[ci]);
             const uint32_t birth = kdiam(colkey);
-            uint64_t meta = hfind(tau);
+            uint32_t app;
+            uint64_t meta = lookup(dim, tau, tv, app);
             WSUB(1);
-            uint32_t app = meta == kNoMetaW ? apparent_owner(dim, tv) : kNoneW;
-            WSUB(2);
             int v = 0;  // 0 = lazy: V == {this column}
             if (meta != kNoMetaW || app != kNoneW) {
                 v_toggle(cp, v);
@@ -822,10 +895,8 @@ struct WideCx {
                     tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInfW;
                     WSUB(4);
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
-                    meta = hfind(tau);
+                    meta = lookup(dim, tau, tv, app);
                     WSUB(1);
-                    app = meta == kNoMetaW ? apparent_owner(dim, tv) : kNoneW;
-                    WSUB(2);
                     if (meta == kNoMetaW && app == kNoneW) break;  // tau is this column's pivot
                     if (++guard > ly.guard) {
                         err |= kEGuard;
