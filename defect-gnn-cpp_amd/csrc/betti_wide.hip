@@ -26,6 +26,9 @@
 
 #include "dgn_internal.hpp"
 
+#ifndef DGN_PV_UNROLL
+#define DGN_PV_UNROLL 2  // V entries evaluated together in the pivot search
+#endif
 #ifndef DGN_WIDE_STEP
 #define DGN_WIDE_STEP 4
 #endif
@@ -801,6 +804,14 @@ struct WideCx {
                 }
                 const int cnt = v - base < kWave ? v - base : kWave;
                 int i = 0;
+#if DGN_PV_UNROLL >= 4
+                for (; i + 3 < cnt; i += 4) {  // four entries' distance reads in flight together
+                    eval(rlw(vl, i), rlw(vd, i));
+                    eval(rlw(vl, i + 1), rlw(vd, i + 1));
+                    eval(rlw(vl, i + 2), rlw(vd, i + 2));
+                    eval(rlw(vl, i + 3), rlw(vd, i + 3));
+                }
+#endif
                 for (; i + 1 < cnt; i += 2) {  // two entries' distance reads in flight together
                     eval(rlw(vl, i), rlw(vd, i));
                     eval(rlw(vl, i + 1), rlw(vd, i + 1));
