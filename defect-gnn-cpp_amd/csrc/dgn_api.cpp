@@ -313,7 +313,7 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
     const int cap = graph_emit_cap(W.max_candidates);
     if (cap == 0)
-        return fail(c, DGN_ERR_UNSUPPORTED, "more than 512 neighbour candidates for one atom (cutoff too large)");
+        return fail(c, DGN_ERR_UNSUPPORTED, "more than 1024 neighbour candidates for one atom (cutoff too large)");
     if (b->num_atoms == 0) return DGN_OK;
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, sizeof(uint32_t), c->stream));

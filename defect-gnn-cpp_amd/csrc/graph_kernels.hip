@@ -1607,6 +1607,7 @@ int graph_emit_cap(uint32_t m) {
     if (m <= 128) return 128;
     if (m <= 256) return 256;
     if (m <= 512) return 512;
+    if (m <= 1024) return 1024;
     return 0;
 }
 
@@ -1698,6 +1699,7 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
         DGN_EMIT(128)
         DGN_EMIT(256)
         DGN_EMIT(512)
+        DGN_EMIT(1024)
         default:
             return hipErrorInvalidValue;
     }

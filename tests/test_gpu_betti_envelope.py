@@ -78,15 +78,15 @@ def test_forced_capacity_retry_all_tiers(ctx, monkeypatch):
 
 @pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
 def test_cloud_above_512_points(ctx):
-    """Complexes of 513..1024 points: the regular wide launch lists them for the retry launch,
-    which runs the rank-coded (BIG) instantiation; a 520- and a 700-point cloud plus a small one
-    in the same batch, against verbatim Ripser."""
+    """Complexes of 513..1024 points: the bucket pass lists them for the retry launch, which runs
+    the rank-coded (BIG) instantiation (126 KB of adjacency LDS at 1,000 points); 1,000-, 700- and
+    520-point clouds plus a small one in the same batch, against verbatim Ripser."""
     rng = np.random.default_rng(43)
-    sizes = [700, 520, 90]
+    sizes = [1000, 700, 520, 90]
     clouds = np.zeros((len(sizes), max(sizes), 3))
     for c, n in enumerate(sizes):
-        clouds[c, :n] = rng.uniform(0, 9.0, size=(n, 3))
-    clouds[1, 10] = clouds[1, 3]  # a duplicate point: zero distance, dim-0 pair not emitted
+        clouds[c, :n] = rng.uniform(0, 9.0 * (n / 700) ** (1 / 3), size=(n, 3))
+    clouds[2, 10] = clouds[2, 3]  # a duplicate point: zero distance, dim-0 pair not emitted
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.6, 1 << 14)
     assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
 

@@ -156,3 +156,19 @@ def test_device_count_emit_full_shard(ctx):
         assert np.array_equal(rp[s * n:(s + 1) * n + 1] - a, nl["row_ptr"])
         assert np.array_equal(col[a:b], nl["col"]) and np.array_equal(dist[a:b], nl["dist"])
         check_rbf(rbf[a:b], nl["dist"], 5.0, 0.1)
+
+
+@pytest.mark.parametrize("k", [20, None])
+def test_fcc256_cutoff_12A_above_512_candidates(ctx, k):
+    """NeighborList(rc = 12): ~580 candidates per atom (the 1,024-candidate emit), CSR bit-exact."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    p = abi.graph_params(r_cutoff=12.0, max_neighbors=k, rbf_cutoff=12.0, rbf_dr=0.1, write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, 12.0, k)
+    if k is None:
+        assert np.diff(rp).max() > 512
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
+    check_rbf(g["rbf"], dist, 12.0, 0.1)
