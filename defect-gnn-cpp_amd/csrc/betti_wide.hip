@@ -70,8 +70,13 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 // rank codes in the complex (order- and equality-preserving, < 2^20; betti_rank_codes) so a
 // simplex key (code << 36) | ~index fits 64 bits (C(1024, 4) < 2^36); code -> f32 via the
 // complex's sorted distances. Otherwise 9-bit vertices and (f32 bits << 32) | ~index keys.
-template <int KW, bool BIG>
+// MODE: kF32 (distances as f32 bits), kC16 (u16 rank codes: 4-byte -> 2-byte matrix for
+// complexes of <= 362 points, C(362, 2) < 2^16), kBig (above).
+constexpr int kF32 = 0, kC16 = 1, kBig = 2;
+template <int KW, int MODE>
 struct WideCx {
+    static constexpr bool BIG = MODE == kBig;
+    static constexpr bool CODED = MODE != kF32;
     static constexpr int kWW = KW;
     static constexpr int VB = BIG ? 10 : 9;            // bits per packed vertex
     static constexpr uint64_t VM = (1ull << VB) - 1;
@@ -102,13 +107,16 @@ struct WideCx {
     float thr;
     uint32_t err;
     int n_d0, n_inf0, n_p1, n_p2;
-    const uint32_t* vals = nullptr;  // BIG: the complex's sorted f32 distances (code -> value)
+    const uint32_t* vals = nullptr;  // CODED: the complex's sorted f32 distances (code -> value)
 
-    __device__ float value(uint32_t dc) const { return BIG ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
+    __device__ float value(uint32_t dc) const { return CODED ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
 
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
-    __device__ uint32_t d(int i, int j) const { return sp<uint32_t>(ly.D)[(int64_t)i * n + j]; }
+    __device__ uint32_t d(int i, int j) const {
+        if (MODE == kC16) return sp<uint16_t>(ly.D)[(int64_t)i * n + j];
+        return sp<uint32_t>(ly.D)[(int64_t)i * n + j];
+    }
     __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
     __device__ bool is_tree(int i, int j) const { return par[i] == j || par[j] == i; }
     __device__ uint32_t sdiam(int dim, uint64_t p) const {  // dim 1: edge, dim 2: triangle
@@ -121,9 +129,13 @@ struct WideCx {
         const int lane = lane_id();
         const float* L = bl.lower + gi * bl.tri_stride;
         uint32_t* D = sp<uint32_t>(ly.D);
-        const uint32_t* Lc = BIG ? bl.rank_codes + slot * bl.rank_stride : nullptr;
+        uint16_t* D16 = sp<uint16_t>(ly.D);
+        const uint32_t* Lc = CODED ? bl.rank_codes + slot * bl.rank_stride : nullptr;
         for (int i = lane; i < n * W; i += kWave) adj[i] = 0ull;
-        for (int i = lane; i < n; i += kWave) D[(int64_t)i * n + i] = 0u;  // 0.0f, or code 0 (BIG: unused)
+        for (int i = lane; i < n; i += kWave) {  // the diagonal is never read as a distance
+            if (MODE == kC16) D16[(int64_t)i * n + i] = 0;
+            else D[(int64_t)i * n + i] = 0u;
+        }
         wave_lds_order();
         for (int i = 1; i < n; ++i) {
             for (int j0 = 0; j0 < i; j0 += kWave) {
@@ -131,9 +143,14 @@ struct WideCx {
                 bool e = false;
                 if (j < i) {
                     const float v = L[c2i(i) + j];
-                    const uint32_t dv = BIG ? Lc[c2i(i) + j] : __float_as_uint(v);
-                    D[(int64_t)i * n + j] = dv;
-                    D[(int64_t)j * n + i] = dv;
+                    const uint32_t dv = CODED ? Lc[c2i(i) + j] : __float_as_uint(v);
+                    if (MODE == kC16) {
+                        D16[(int64_t)i * n + j] = (uint16_t)dv;
+                        D16[(int64_t)j * n + i] = (uint16_t)dv;
+                    } else {
+                        D[(int64_t)i * n + j] = dv;
+                        D[(int64_t)j * n + i] = dv;
+                    }
                     e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
                 }
                 const uint64_t b = ballot(e);
@@ -1048,7 +1065,7 @@ struct WideCx {
     }
 };
 
-template <int KW, bool BIG>
+template <int KW, int MODE>
 __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
     // [nmax] u16, the dequeue slot
@@ -1077,8 +1094,8 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
             if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
         } else {
-            WideCx<KW, BIG> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
-            if (BIG) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+            WideCx<KW, MODE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+            if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
             cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
         }
     }
@@ -1088,13 +1105,18 @@ int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
 // the instantiation for complexes of up to nmax points: 2, 4, 6 or 8 bitset words per vertex
 using WideKernel = void (*)(BettiLaunch, WideLayout);
-WideKernel wide_kernel_for(int nmax) {
+WideKernel wide_kernel_for(int nmax, bool c16) {
     const int w = (nmax + 63) / 64;
-    if (w <= 2) return betti_wide_kernel<2, false>;
-    if (w <= 4) return betti_wide_kernel<4, false>;
-    if (w <= 6) return betti_wide_kernel<6, false>;
-    if (w <= 8) return betti_wide_kernel<8, false>;
-    return betti_wide_kernel<16, true>;  // 513..1024 points: rank-coded distances (BIG)
+    if (c16 && nmax <= kC16MaxPoints) {  // u16 rank codes (betti_rank_codes before the launch)
+        if (w <= 2) return betti_wide_kernel<2, kC16>;
+        if (w <= 4) return betti_wide_kernel<4, kC16>;
+        return betti_wide_kernel<6, kC16>;
+    }
+    if (w <= 2) return betti_wide_kernel<2, kF32>;
+    if (w <= 4) return betti_wide_kernel<4, kF32>;
+    if (w <= 6) return betti_wide_kernel<6, kF32>;
+    if (w <= 8) return betti_wide_kernel<8, kF32>;
+    return betti_wide_kernel<16, kBig>;  // 513..1024 points: rank-coded distances (BIG)
 }
 
 size_t wide_lds_bytes(int nmax) {
@@ -1160,7 +1182,7 @@ int betti_wide_resident_waves(int device, int nmax) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax), kWave, wide_lds_bytes(nmax)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, false), kWave, wide_lds_bytes(nmax)) !=
             hipSuccess ||
         per_cu <= 0)
         per_cu = 2;
@@ -1169,7 +1191,8 @@ int betti_wide_resident_waves(int device, int nmax) {
 
 hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
     if (waves <= 0) return hipSuccess;
-    hipLaunchKernelGGL(wide_kernel_for(l.nmax), dim3((unsigned)waves), dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
+    hipLaunchKernelGGL(wide_kernel_for(l.nmax, b.rank_codes != nullptr && l.nmax <= kC16MaxPoints), dim3((unsigned)waves),
+                       dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
     return hipGetLastError();
 }
 

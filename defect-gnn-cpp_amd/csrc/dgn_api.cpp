@@ -112,7 +112,7 @@ struct dgn_ctx {
     HostScalars* host = nullptr;  // pinned
     bool emit_pending = false;    // an emit's error flag is on its way to host->emit_flag
     // betti workspace
-    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big, b_rank, b_rscal;
+    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big, b_rank, b_rscal, b_rank16, b_rscal16;
     int betti_slots = 0;
     bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
@@ -463,10 +463,53 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.counts = counts ? counts + 4 * c0 : nullptr;
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
         HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 7 * sizeof(uint32_t), c->stream));
+        // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
+        // the scattered walk and pivot-search reads miss on): the narrow launches and the bucket
+        // pass first, then per slice of the wide list its codes (betti_rank_codes) and a wide launch
+        static const bool c16_env = [] {
+            const char* e = std::getenv("DGN_WIDE_C16");  // A/B: 0 = f32 distances
+            return !(e && e[0] == '0');
+        }();
+        const bool c16 = c16_env && max_points > 64 && max_points <= kC16MaxPoints;
         {
             TimedLaunch t(c, "betti_vr", bytes, 0.0);
-            HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots, max_points > 64 ? &wl : nullptr,
-                                    wide_waves, &fork));
+            HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots,
+                                    max_points > 64 && !c16 ? &wl : nullptr, wide_waves, &fork));
+            if (c16) {
+                HIP_TRY(c, hipMemcpyAsync(&c->host->s.wide_len, &sc->wide_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                          c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                const int64_t nwide = c->host->s.wide_len;
+                const int64_t rstride = ((int64_t)max_points * (max_points - 1) / 2 + 63) / 64 * 64;
+                const int64_t slice =
+                    std::max<int64_t>(1, std::min<int64_t>(nwide, (int64_t(16) << 30) / (20 * rstride)));
+                const size_t tmp_bytes = betti_rank_temp_bytes(slice, rstride);
+                HIP_TRY(c, c->b_rank16.ensure(8 * (size_t)slice * rstride + tmp_bytes));
+                const int64_t nsl = (nwide + slice - 1) / slice;
+                HIP_TRY(c, c->b_rscal16.ensure(sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(nsl, 1)));
+                std::vector<uint32_t> lens((size_t)std::max<int64_t>(nsl, 1));
+                for (int64_t q = 0; q < nsl; ++q) lens[q] = (uint32_t)std::min<int64_t>(slice, nwide - q * slice);
+                uint32_t* sl = c->b_rscal16.as<uint32_t>();
+                HIP_TRY(c, hipMemsetAsync(sl, 0, sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(nsl, 1), c->stream));
+                for (int64_t q = 0; q < nsl; ++q)
+                    HIP_TRY(c, hipMemcpyAsync(sl + 2 * q, &lens[q], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+                uint32_t* codes = c->b_rank16.as<uint32_t>();
+                uint32_t* sorted = codes + slice * rstride;
+                for (int64_t q = 0; q < nsl; ++q) {
+                    BettiLaunch wb = pb;
+                    wb.wide_list = c->b_wlist.as<int32_t>() + q * slice;
+                    wb.wide_len = sl + 2 * q;
+                    wb.wide_queue = sl + 2 * q + 1;
+                    HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, wb.wide_list,
+                                                (int64_t)lens[q], rstride, codes, sorted, sorted + slice * rstride,
+                                                tmp_bytes));
+                    wb.rank_codes = codes;
+                    wb.rank_sorted = sorted;
+                    wb.rank_stride = rstride;
+                    HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
+                }
+                HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope
+            }
         }
         // complexes whose reduction outgrew a kernel's workspace (the reference's Ripser has no
         // caps, ripser.cpp:514-1269): reduced again with the big wide layout
@@ -499,6 +542,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             HIP_TRY(c, c->b_rscal.ensure(sizeof(uint32_t) * 2 * (size_t)((nretry + slice - 1) / slice)));
         }
         BettiLaunch rb = pb;
+        rb.rank_codes = nullptr;  // set per slice below when coded
+        rb.rank_sorted = nullptr;
         rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
         rb.retry_len = nullptr;
         rb.force_retry = 0;

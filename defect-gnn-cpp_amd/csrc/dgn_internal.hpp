@@ -124,6 +124,7 @@ struct BettiLaunch {
 // launch after betti_rank_codes
 constexpr int kWideMaxPoints = 1024;
 constexpr int kWideRegular = 512;
+constexpr int kC16MaxPoints = 362;  // C(362, 2) < 2^16: u16 rank codes (wide launch)
 struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
