@@ -12,7 +12,7 @@ OUT=gpurun_out/prof_$R
 mkdir -p "$OUT"
 cd "$(dirname "$0")/.." 
 export TMPDIR=/tmp
-BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 $BENCH > "$OUT/trace_bench.json" 2> "$OUT/trace_bench.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
