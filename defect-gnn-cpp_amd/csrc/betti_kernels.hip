@@ -1037,7 +1037,6 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
-            if (bl.force_retry) cx.err |= kErrNA;
             const uint32_t err = uni(cx.err);
             if (err && bl.retry_list && (err & kErrCapacity) == err) {
                 // workspace overflow: the capacity-retry launch (betti_wide_kernel, big layout)

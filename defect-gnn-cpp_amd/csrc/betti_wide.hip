@@ -982,7 +982,6 @@ struct WideCx {
         const int lane = lane_id();
         double* feat = bl.features ? bl.features + 35 * gi : nullptr;
         if (n_p1 > ly.p_cap || n_p2 > ly.p_cap) err |= kEPairs;
-        if (bl.force_retry && bl.retry_list) err |= kENA;
         if (err && bl.retry_list && (err & kECapacity) == err) {
             // workspace overflow: listed for the capacity-retry launch (betti_wide_layout big),
             // which writes this complex's outputs

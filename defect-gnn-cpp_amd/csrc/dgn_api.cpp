@@ -511,6 +511,18 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope
             }
         }
+        if (pb.force_retry) {
+            // test knob (no kernel checks it: a per-complex flag read cost 0.8 % of the narrow
+            // launch): every complex of the pass is listed for the retry launch, which overwrites
+            // its outputs
+            std::vector<int32_t> all((size_t)cnt);
+            for (int64_t i = 0; i < cnt; ++i) all[(size_t)i] = (int32_t)i;
+            const uint32_t n32 = (uint32_t)cnt;
+            HIP_TRY(c, hipMemcpyAsync(c->b_rlist.p, all.data(), sizeof(int32_t) * (size_t)cnt, hipMemcpyHostToDevice,
+                                      c->stream));
+            HIP_TRY(c, hipMemcpyAsync(&sc->retry_len, &n32, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
         // complexes whose reduction outgrew a kernel's workspace (the reference's Ripser has no
         // caps, ripser.cpp:514-1269): reduced again with the big wide layout
         HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
