@@ -28,6 +28,8 @@
 //     dim>=1 classes are not emitted, ripser.cpp:1209-1225).
 //   * persistent grid, chunked dynamic dequeue; per-wave global scratch for reduced columns
 //     and pair lists.
+#include <atomic>
+
 #include "dgn_internal.hpp"
 
 namespace dgn {
@@ -1173,27 +1175,31 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
 
 // device facts for the persistent grids, queried once per device (hipGetDeviceProperties is a
 // slow host call and every Betti call launches up to three grids)
+// (relaxed atomics: contexts on different host threads may fill a slot concurrently; every
+// writer stores the same value)
 static int cu_count(int dev) {
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64];
     if (dev < 0 || dev >= 64) return 256;
-    if (cus[dev] == 0) {
+    int v = cus[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
         hipDeviceProp_t prop;
-        cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+        v = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+        cus[dev].store(v, std::memory_order_relaxed);
     }
-    return cus[dev];
+    return v;
 }
 
 template <int NP>
 static int grid_np(int grid_waves, int64_t max_items) {
     int dev = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
-    static int occ[64] = {0};
-    if (dev >= 0 && dev < 64 && occ[dev] > 0) {
-        per_cu = occ[dev];
+    static std::atomic<int> occ[64];
+    if (dev >= 0 && dev < 64 && occ[dev].load(std::memory_order_relaxed) > 0) {
+        per_cu = occ[dev].load(std::memory_order_relaxed);
     } else {
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, 0);
         if (e != hipSuccess || per_cu <= 0) per_cu = 4;
-        if (dev >= 0 && dev < 64) occ[dev] = per_cu;
+        if (dev >= 0 && dev < 64) occ[dev].store(per_cu, std::memory_order_relaxed);
     }
     int grid = cu_count(dev) * per_cu;
     if (grid > grid_waves) grid = grid_waves;
