@@ -23,6 +23,7 @@
 // only, essential dim >= 1 classes are not emitted (ripser.cpp:1209-1225, 1240). The pairing
 // of a total order is unique, so the emitted multiset equals Ripser's.
 #include <algorithm>
+#include <cstdlib>
 
 #include "dgn_internal.hpp"
 
@@ -1065,7 +1066,7 @@ struct WideCx {
 };
 
 template <int KW, int MODE>
-__global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
+__device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const WideLayout& ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
     // [nmax] u16, the dequeue slot
     extern __shared__ uint64_t wide_lds[];
@@ -1100,6 +1101,21 @@ __global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideL
     }
 }
 
+template <int KW, int MODE>
+__global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
+    betti_wide_body<KW, MODE>(bl, ly);
+}
+#ifndef DGN_WIDE_C16_WAVES
+#define DGN_WIDE_C16_WAVES 3  // waves per SIMD the u16-code instantiations are compiled for
+#endif
+// the u16-code instantiations (the 10 A path) with a register budget for DGN_WIDE_C16_WAVES waves
+// per SIMD: resident waves are what this latency-bound kernel scales with
+template <int KW>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(DGN_WIDE_C16_WAVES, DGN_WIDE_C16_WAVES)))
+void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
+    betti_wide_body<KW, kC16>(bl, ly);
+}
+
 int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
 // the instantiation for complexes of up to nmax points: 2, 4, 6 or 8 bitset words per vertex
@@ -1107,9 +1123,9 @@ using WideKernel = void (*)(BettiLaunch, WideLayout);
 WideKernel wide_kernel_for(int nmax, bool c16) {
     const int w = (nmax + 63) / 64;
     if (c16 && nmax <= kC16MaxPoints) {  // u16 rank codes (betti_rank_codes before the launch)
-        if (w <= 2) return betti_wide_kernel<2, kC16>;
-        if (w <= 4) return betti_wide_kernel<4, kC16>;
-        return betti_wide_kernel<6, kC16>;
+        if (w <= 2) return betti_wide_kernel_c16<2>;
+        if (w <= 4) return betti_wide_kernel_c16<4>;
+        return betti_wide_kernel_c16<6>;
     }
     if (w <= 2) return betti_wide_kernel<2, kF32>;
     if (w <= 4) return betti_wide_kernel<4, kF32>;
@@ -1176,12 +1192,20 @@ hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves
     return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
 }
 
+bool betti_wide_c16_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("DGN_WIDE_C16");  // A/B: 0 = f32 distances
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // waves of betti_wide_kernel resident on the whole device for complexes of up to nmax points
-int betti_wide_resident_waves(int device, int nmax) {
+int betti_wide_resident_waves(int device, int nmax, bool c16) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, false), kWave, wide_lds_bytes(nmax)) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, c16), kWave, wide_lds_bytes(nmax)) !=
             hipSuccess ||
         per_cu <= 0)
         per_cu = 2;

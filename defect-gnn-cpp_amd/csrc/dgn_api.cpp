@@ -401,7 +401,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
-        const int64_t resident = betti_wide_resident_waves(c->device, wide_nmax);
+        const int64_t resident = betti_wide_resident_waves(
+            c->device, wide_nmax, betti_wide_c16_enabled() && wide_nmax <= kC16MaxPoints);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         if (const char* ev = std::getenv("DGN_WIDE_WAVES")) {  // A/B experiments only
             const int w = std::atoi(ev);
@@ -466,11 +467,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
         // the scattered walk and pivot-search reads miss on): the narrow launches and the bucket
         // pass first, then per slice of the wide list its codes (betti_rank_codes) and a wide launch
-        static const bool c16_env = [] {
-            const char* e = std::getenv("DGN_WIDE_C16");  // A/B: 0 = f32 distances
-            return !(e && e[0] == '0');
-        }();
-        const bool c16 = c16_env && max_points > 64 && max_points <= kC16MaxPoints;
+        const bool c16 = betti_wide_c16_enabled() && max_points > 64 && max_points <= kC16MaxPoints;
         {
             TimedLaunch t(c, "betti_vr", bytes, 0.0);
             HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots,
