@@ -63,6 +63,7 @@ struct PendingEvent {
 struct Scalars {  // device-side scalars, one allocation
     int64_t total;
     unsigned long long sum_sq;  // sum over atoms of (candidates + 1)^2
+    unsigned long long sum_m;   // sum over atoms of candidates (every neighbour within rc)
     uint32_t max_candidates;
     uint32_t max_natoms;        // largest structure of the batch (prep)
     uint32_t graph_flag;        // graph error bits kGErr* (prep, emit, Betti search)
@@ -81,6 +82,7 @@ struct Scalars {  // device-side scalars, one allocation
 struct GraphWork {
     DevBuf meta, counts, block_sums, block_aux, atom_struct, cell_start, cell_pos, mask, weight;
     bool have = false;
+    bool has_weight = false;  // weight[] holds the 1/count(species) Betti weights of this batch
     const double* pos = nullptr;
     int64_t atoms = -1, structs = -1;
     double rc = 0, eps = 0;
@@ -88,6 +90,7 @@ struct GraphWork {
     uint32_t max_candidates = 0, max_natoms = 0;
     int64_t edges = 0;
     double sum_sq = 0;
+    double sum_m = 0;  // neighbours within rc over the batch (the K = inf edge count)
 };
 
 // host-pinned mirror: the scalars after a count pass, and the emit's deferred error flag
@@ -254,12 +257,15 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     HIP_TRY(c, W.meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
     HIP_TRY(c, W.counts.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
-    HIP_TRY(c, W.block_aux.ensure(3 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, W.block_aux.ensure(4 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
     HIP_TRY(c, W.atom_struct.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.cell_start.ensure(sizeof(int32_t) * (size_t)(A + B + 1)));
     HIP_TRY(c, W.cell_pos.ensure(sizeof(double4) * A1));
     HIP_TRY(c, W.mask.ensure(sizeof(uint64_t) * kMaskWords * A1));
-    const bool want_weight = betti && b->species;
+    // the Betti weights ride along with any pass that has species, so a Betti pass at the same
+    // cutoff can reuse this one (betti_impl)
+    const bool want_weight = b->species != nullptr;
+    (void)betti;
     if (want_weight) HIP_TRY(c, W.weight.ensure(sizeof(double) * A1));
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
     Scalars* sc = c->scalars.as<Scalars>();
@@ -283,7 +289,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     {
         TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 32, 0);
         HIP_TRY(c, launch_block_scan(c->stream, W.block_sums.as<int64_t>(), W.block_aux.as<uint64_t>(), nblocks,
-                                     &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms));
+                                     &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms, &sc->sum_m));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->s, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -302,6 +308,8 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     W.max_natoms = c->host->s.max_natoms;
     W.edges = c->host->s.total;
     W.sum_sq = (double)c->host->s.sum_sq;
+    W.sum_m = (double)c->host->s.sum_m;
+    W.has_weight = want_weight;
     if (num_edges) *num_edges = W.edges;
     return DGN_OK;
 }
@@ -347,18 +355,25 @@ int check_emit_flag(dgn_ctx* c) {
 
 int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int32_t* counts, const double* clouds,
                const int32_t* npoints, int32_t cloud_stride, int64_t num_clouds, float* pairs_out, int32_t pair_cap,
-               const float* lower = nullptr) {
+               const float* lower = nullptr, bool reuse_graph = false) {
     const bool given = clouds || lower;
     const int64_t A = given ? num_clouds : b->num_atoms;
+    auto nw = [&]() -> GraphWork& { return reuse_graph ? c->gw : c->bw; };
     if (A == 0) return DGN_OK;
     int max_points = cloud_stride;
     if (!given) {
         // NeighborList(rc, SIZE_MAX) counts (betti_features.cpp:107): the largest local complex,
         // sum n^2 for the byte accounting, the per-atom weights
-        int64_t E = 0;
-        int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E, true);
-        if (st) return st;
-        max_points = (int)c->bw.max_candidates + 1;
+        // dgn_dev_graph_betti: the graph pass's count at the same cutoff already holds every
+        // neighbour within rc (NeighborList(rc, K) and NeighborList(rc, SIZE_MAX) see the same
+        // candidates, neighbor_list.cpp:27-66); its per-atom counts, hit masks, cell lists and
+        // weights serve the Betti search unchanged
+        if (!reuse_graph) {
+            int64_t E = 0;
+            int st = graph_count_impl(c, b, rc, UINT64_MAX, 1e-10, &E, true);
+            if (st) return st;
+        }
+        max_points = (int)nw().max_candidates + 1;
     }
     if (max_points > betti_max_points())
         return fail(c, DGN_ERR_UNSUPPORTED,
@@ -602,9 +617,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         HIP_TRY(c, c->b_np.ensure(sizeof(int32_t) * (size_t)chunk));
         HIP_TRY(c, c->b_w.ensure(sizeof(double) * (size_t)chunk));
         // per-complex averages over the batch: points n (sum n = E + A), sum n^2 from the count pass
-        const double En = given ? 0.0 : (double)c->bw.edges, An = (double)A;
-        const double sum_n2 = given ? 0.0 : c->bw.sum_sq;
-        const GraphLaunch g = given ? GraphLaunch{} : graph_launch(c->bw, b, rc, 1e-10, UINT64_MAX, true);
+        const double En = given ? 0.0 : nw().sum_m, An = (double)A;
+        const double sum_n2 = given ? 0.0 : nw().sum_sq;
+        const GraphLaunch g = given ? GraphLaunch{} : graph_launch(nw(), b, rc, 1e-10, UINT64_MAX, true);
         for (int64_t c0 = 0; c0 < A; c0 += chunk) {
             const int64_t cnt = std::min<int64_t>(chunk, A - c0);
             const double f = (double)cnt / An;
@@ -620,13 +635,13 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                     HIP_TRY(c, launch_betti_dist(c->stream, db, dl));
                 } else {
                     HIP_TRY(c, launch_betti_dist_search(c->stream, g, c0, cnt, max_points, tri_stride,
-                                                        c->bw.counts.as<int32_t>(), c->b_lower.as<float>(),
+                                                        nw().counts.as<int32_t>(), c->b_lower.as<float>(),
                                                         c->b_np.as<int32_t>(), &sc->graph_flag));
                 }
             }
             // Betti pass: triangles in, 35 f64 + 4 i32 out
             const double bytes = given ? 0.0 : f * (2 * (sum_n2 - (En + An)) + 12 * An + An * (35 * 8 + 16));
-            const double* w = given ? c->b_w.as<double>() : (b->species ? c->bw.weight.as<double>() + c0 : nullptr);
+            const double* w = given ? c->b_w.as<double>() : (b->species ? nw().weight.as<double>() + c0 : nullptr);
             int st = vr_pass(c0, cnt, c->b_lower.as<float>(), tri_stride, c->b_np.as<int32_t>(), w, bytes);
             if (st) return st;
         }
@@ -893,6 +908,20 @@ int dgn_dev_betti(dgn_ctx* c, const dgn_batch* b, const dgn_betti_params* p, dou
         return fail(c, DGN_ERR_ARG, "dgn_dev_betti: bad args");
     HIP_TRY(c, hipSetDevice(c->device));
     return betti_impl(c, b, p->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0);
+}
+
+int dgn_dev_graph_betti(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* p, int64_t* row_ptr,
+                        const dgn_graph_out* o, const dgn_betti_params* bp, double* features, int32_t* counts) {
+    if (!c || !p || !bp || !batch_ok(b) || !b->species || !features || !(bp->r_cutoff > 0))
+        return fail(c, DGN_ERR_ARG, "dgn_dev_graph_betti: bad args");
+    if (p->r_cutoff != c->gw.rc || p->max_neighbors != c->gw.k || p->epsilon != c->gw.eps || !c->gw.have ||
+        c->gw.pos != b->positions || c->gw.atoms != b->num_atoms)
+        return fail(c, DGN_ERR_ARG, "dgn_dev_graph_betti: no matching dgn_dev_graph_count on this context");
+    int st = dgn_dev_graph_emit(c, b, p, row_ptr, o);
+    if (st) return st;
+    // one neighbour count for both passes when the cutoffs agree (the bench's config: rc 5 / 5)
+    const bool reuse = bp->r_cutoff == p->r_cutoff && p->epsilon == 1e-10 && c->gw.has_weight;
+    return betti_impl(c, b, bp->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0, nullptr, reuse);
 }
 
 int dgn_dev_node_features(dgn_ctx* c, const dgn_batch* b, const double* embed, int32_t num_keys, int32_t D,

@@ -51,14 +51,15 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
                                   const int32_t* species, int64_t num_structures, double rc, StructMeta* meta,
                                   int32_t* atom_struct, int32_t* cell_start, double4* cell_pos, double* weight,
                                   uint32_t* error_flag);
-// per-atom kept counts min(m, kmax); per block: block_sums[b] and block_aux[3b] = max candidates m,
-// block_aux[3b+1] = sum over atoms of (m + 1)^2, block_aux[3b+2] = largest structure;
+// per-atom hit counts m (every neighbour within rc; the emit keeps min(m, kmax)); per block:
+// block_sums[b] = sum of min(m, kmax) and block_aux[4b] = max m, block_aux[4b+1] = sum over atoms
+// of (m + 1)^2, block_aux[4b+2] = largest structure, block_aux[4b+3] = sum of m;
 // mask_out (optional) [A][kMaskWords]: exact hits of staged one-image structures
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
                               uint64_t* block_aux, uint64_t* mask_out);
 hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t* block_aux, int64_t nblocks,
                              int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq,
-                             uint32_t* max_natoms);
+                             uint32_t* max_natoms, unsigned long long* sum_m);
 // Fused emit: each block re-runs the search for its atoms, ranks, writes row_ptr / col / dist /
 // disp and the RBF. cap >= max candidates of the count pass (64..512); stage = atoms staged in LDS
 // (max structure size if <= kStage, else 0).

@@ -721,14 +721,14 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     __shared__ int32_t cnt_s[kQA], nw_s[kQA];        // block outputs, written at the end (no global
     __shared__ uint64_t mask_s[kQA][kMaskWords];     // memory inside the per-query loop)
     __shared__ int64_t wsum[kW];
-    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW];
+    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW], wm[kW];
     const StageView st = make_stage(stage_mem, kStage, offt_s);
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
     const int64_t g0 = (int64_t)blockIdx.x * kQA;
     int64_t my_sum = 0;
     uint32_t my_max = 0, my_nat = 0;
-    uint64_t my_sq = 0;
+    uint64_t my_sq = 0, my_m = 0;
     for_block_atoms(g, st, 0, g.num_atoms, blockIdx.x, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         double q[3];
@@ -743,10 +743,11 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
         }
         const int64_t c = (uint64_t)m < g.kmax ? (int64_t)m : (int64_t)g.kmax;
         if (lane == 0) {
-            cnt_s[t] = (int32_t)c;
+            cnt_s[t] = (int32_t)m;  // every hit: the emit keeps min(m, kmax), a Betti pass at this rc reuses m
             nw_s[t] = nw;
         }
         my_sum += c;
+        my_m += (uint64_t)m;
         my_max = (uint32_t)m > my_max ? (uint32_t)m : my_max;
         my_nat = (uint32_t)M.natoms > my_nat ? (uint32_t)M.natoms : my_nat;
         my_sq += (uint64_t)(m + 1) * (uint64_t)(m + 1);  // local-complex n^2
@@ -756,6 +757,7 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
         wmax[w] = my_max;
         wsq[w] = my_sq;
         wnat[w] = my_nat;
+        wm[w] = my_m;
     }
     __syncthreads();
     const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
@@ -767,17 +769,19 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
         }
     if (threadIdx.x == 0) {
         int64_t s = 0;
-        uint64_t mx = 0, sq = 0, nat = 0;
+        uint64_t mx = 0, sq = 0, nat = 0, sm = 0;
         for (int k = 0; k < kW; ++k) {
             s += wsum[k];
+            sm += wm[k];
             mx = wmax[k] > mx ? wmax[k] : mx;
             nat = wnat[k] > nat ? wnat[k] : nat;
             sq += wsq[k];
         }
         block_sums[blockIdx.x] = s;
-        block_aux[3 * blockIdx.x] = mx;
-        block_aux[3 * blockIdx.x + 1] = sq;
-        block_aux[3 * blockIdx.x + 2] = nat;
+        block_aux[4 * blockIdx.x] = mx;
+        block_aux[4 * blockIdx.x + 1] = sq;
+        block_aux[4 * blockIdx.x + 2] = nat;
+        block_aux[4 * blockIdx.x + 3] = sm;
     }
 }
 
@@ -790,18 +794,21 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
                                                                   int64_t* __restrict__ total,
                                                                   uint32_t* __restrict__ max_candidates,
                                                                   unsigned long long* __restrict__ sum_sq,
-                                                                  uint32_t* __restrict__ max_natoms) {
+                                                                  uint32_t* __restrict__ max_natoms,
+                                                                  unsigned long long* __restrict__ sum_m) {
     __shared__ int64_t wtot[kScanThreads / kWave];
-    __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave], wna[kScanThreads / kWave];
+    __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave], wna[kScanThreads / kWave],
+        wsm[kScanThreads / kWave];
     const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
     __shared__ int64_t carry_s;
     if (tid == 0) carry_s = 0;
     // reductions of the block aux words: coalesced, independent loads
-    uint64_t mx = 0, sq = 0, na = 0;
+    uint64_t mx = 0, sq = 0, na = 0, sm = 0;
     for (int64_t i = tid; i < n; i += kScanThreads) {
-        mx = aux[3 * i] > mx ? aux[3 * i] : mx;
-        sq += aux[3 * i + 1];
-        na = aux[3 * i + 2] > na ? aux[3 * i + 2] : na;
+        mx = aux[4 * i] > mx ? aux[4 * i] : mx;
+        sq += aux[4 * i + 1];
+        na = aux[4 * i + 2] > na ? aux[4 * i + 2] : na;
+        sm += aux[4 * i + 3];
     }
     __syncthreads();
     // exclusive scan, 8 consecutive sums per thread (two 32-byte loads per lane: coalesced), 8192
@@ -841,22 +848,26 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
     mx = wave_max(mx);
     sq = wave_sum(sq);
     na = wave_max(na);
+    sm = wave_sum(sm);
     if (lane == 0) {
         wmx[w] = mx;
         wsq[w] = sq;
         wna[w] = na;
+        wsm[w] = sm;
     }
     __syncthreads();
     if (tid == 0) {
-        uint64_t m = 0, s = 0, a = 0;
+        uint64_t m = 0, s = 0, a = 0, t = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) {
             m = wmx[k] > m ? wmx[k] : m;
             s += wsq[k];
             a = wna[k] > a ? wna[k] : a;
+            t += wsm[k];
         }
         *max_candidates = (uint32_t)m;
         *sum_sq = s;
         *max_natoms = (uint32_t)a;
+        *sum_m = t;
     }
 }
 
@@ -1245,7 +1256,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         __syncthreads();
         // the tile's own rows only: row_ptr[g0 + nq] belongs to the next tile, whose rows may be
         // written by this same launch
-        const int64_t e0 = row_ptr[g0], e1 = row_ptr[g0 + nq - 1] + counts[g0 + nq - 1];
+        const int64_t e0 = row_ptr[g0], e1 = row_ptr[g0 + nq - 1] + min(counts[g0 + nq - 1], K);
         const int ne = (int)(e1 - e0);
         if (!rows_in_lds) {  // RBF tile of an earlier launch's rows
             for (int i = threadIdx.x; i < ne; i += kGraphBlock) dl[i] = dist[e0 + i];
@@ -1273,7 +1284,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     // local scan of this block's counts -> row starts (and row_ptr); kQA == one wave
     if (w == 0) {
         const int64_t gi = g0 + lane;
-        const int64_t c = gi < g.num_atoms ? counts[gi] : 0;
+        const int64_t c = gi < g.num_atoms ? min(counts[gi], K) : 0;  // kept rows: min(m, max_neighbors)
         const int64_t inc = wave_inclusive_sum(c);
         const int64_t start = block_offsets[tile] + inc - c;
         row_start[lane] = start;
@@ -1596,9 +1607,10 @@ hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* coun
 }
 
 hipError_t launch_block_scan(hipStream_t s, int64_t* v, const uint64_t* aux, int64_t n, int64_t* total,
-                             uint32_t* max_candidates, unsigned long long* sum_sq, uint32_t* max_natoms) {
+                             uint32_t* max_candidates, unsigned long long* sum_sq, uint32_t* max_natoms,
+                             unsigned long long* sum_m) {
     hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, v, aux, n, total, max_candidates,
-                       sum_sq, max_natoms);
+                       sum_sq, max_natoms, sum_m);
     return hipGetLastError();
 }
 

@@ -22,7 +22,7 @@ EXPORTS = [
     "dgn_graph_params_default", "dgn_rbf_bins", "dgn_dev_graph_count", "dgn_dev_graph_emit", "dgn_host_graph",
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
-    "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free",
+    "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch",
 ]
 
@@ -116,6 +116,9 @@ def lib():
     L.dgn_host_rbf.argtypes = [vp, vp, i64, dbl, dbl, i32, i32, vp]
     if hasattr(L, "dgn_dev_node_features"):  # absent from older A/B builds
         L.dgn_dev_node_features.argtypes = [vp, C.POINTER(Batch), vp, i32, i32, vp, vp, vp, i32, vp]
+    if hasattr(L, "dgn_dev_graph_betti"):  # absent from older A/B builds
+        L.dgn_dev_graph_betti.argtypes = [vp, C.POINTER(Batch), C.POINTER(GraphParams), vp, C.POINTER(GraphOut),
+                                          C.POINTER(BettiParams), vp, vp]
     if hasattr(L, "dgn_dev_edge_arrays"):  # absent from older A/B builds
         L.dgn_dev_edge_arrays.argtypes = [vp, C.POINTER(Batch), vp, vp, vp, vp, vp, vp, vp, vp]
         L.dgn_host_edge_arrays.argtypes = [vp, C.POINTER(Batch), dbl, C.c_uint64, dbl, C.POINTER(C.POINTER(EdgeArrays))]
@@ -335,6 +338,21 @@ class Context:
         o.rbf = _ptr(rbf)
         self._check(lib().dgn_dev_graph_emit(self.h, C.byref(b), C.byref(params), _ptr(row_ptr), C.byref(o)),
                     "dgn_dev_graph_emit")
+
+    def dev_graph_betti(self, batch: dict, params: GraphParams, row_ptr, col, dist, disp, rbf, r_cutoff: float,
+                        features, counts=None):
+        """dgn_dev_graph_emit + dgn_dev_betti after a dgn_dev_graph_count, sharing the count when the
+        cutoffs agree."""
+        b = make_batch(batch)
+        o = GraphOut()
+        o.col_idx = _ptr(col)
+        o.distance = _ptr(dist)
+        o.displacement = _ptr(disp)
+        o.rbf = _ptr(rbf)
+        p = BettiParams()
+        p.r_cutoff = r_cutoff
+        self._check(lib().dgn_dev_graph_betti(self.h, C.byref(b), C.byref(params), _ptr(row_ptr), C.byref(o),
+                                              C.byref(p), _ptr(features), _ptr(counts)), "dgn_dev_graph_betti")
 
     def dev_betti(self, batch: dict, r_cutoff: float, features, counts=None):
         b = make_batch(batch)

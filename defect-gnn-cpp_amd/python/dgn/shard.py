@@ -59,15 +59,21 @@ class Shard:
         self.out.update(feat=torch.empty((self.A, 35), dtype=torch.float64, device=self.dev),
                         counts=torch.empty((self.A, 4), dtype=torch.int32, device=self.dev))
 
-    def step(self, ctx, gp, betti_rc: float, betti: bool = True, graph: bool = True):
+    def step(self, ctx, gp, betti_rc: float, betti: bool = True, graph: bool = True, fused: bool = True):
+        """graph: NeighborList count + emit (CSR + RBF); betti: the Betti pass. Both with fused:
+        dgn_dev_graph_betti, which shares the neighbour count when the cutoffs agree."""
+        o = self.out
         if graph:
             e = ctx.dev_graph_count(self.batch, gp)
             if e != self.E:
                 raise RuntimeError(f"edge count changed between steps: {e} != {self.E}")
-            o = self.out
+            if betti and fused:
+                ctx.dev_graph_betti(self.batch, gp, o["row_ptr"], o["col"], o["dist"], None, o["rbf"], betti_rc,
+                                    o["feat"], o["counts"])
+                return
             ctx.dev_graph_emit(self.batch, gp, o["row_ptr"], o["col"], o["dist"], None, o["rbf"])
         if betti:
-            ctx.dev_betti(self.batch, betti_rc, self.out["feat"], self.out["counts"])
+            ctx.dev_betti(self.batch, betti_rc, o["feat"], o["counts"])
 
     def results(self) -> dict:
         """Host copies of every output buffer (row_ptr local to the shard)."""

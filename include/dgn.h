@@ -146,6 +146,16 @@ int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* 
 int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
                    double* features, int32_t* counts);
 
+/* Fused step (device, async except for the Betti pass's final flag read): dgn_dev_graph_emit of a
+ * preceding dgn_dev_graph_count, then dgn_dev_betti on the same batch. When the Betti cutoff equals
+ * the graph cutoff (and epsilon is the default 1e-10) the Betti pass reuses the graph count's
+ * per-atom neighbour counts and hit masks instead of searching a third time: CrystalGraph's
+ * NeighborList(rc, K) and compute_structure_betti_features' NeighborList(rc, SIZE_MAX)
+ * (betti_features.cpp:107) enumerate the same candidates. The positions must not change between
+ * the count and this call (as for dgn_dev_graph_emit). */
+int dgn_dev_graph_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_graph_params* p, int64_t* row_ptr,
+                        const dgn_graph_out* out, const dgn_betti_params* bp, double* features, int32_t* counts);
+
 /* ---- node features + topological block (CrystalGraph node_features) --------
  * Device pointers, asynchronous on the context's stream. out: [A][D + k] f64 row-major, row i =
  * embed[species[i]] (the species-keyed embedding gather of crystal_graph.cpp:19-21; embed is
