@@ -1435,8 +1435,16 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 // values of a filtration do not depend on its tie-breaking order), so the rows keep the search's
 // order instead of the sorted one. Writes the f32 lower triangle (MFMA Gram product) + npoints.
 // ------------------------------------------------------------------------------------------
+// The Betti search + MFMA distance kernel writes ~1 KB of triangle per complex with little reuse:
+// compiled for 4 waves per SIMD (128 VGPRs, a few spills) it keeps more stores in flight than at
+// its natural 161 VGPRs (3 waves): 7.6 -> 5.9 ms per config-4 shard (tools/ab_dist.sh)
+// (the 64-point instantiation; the wide ones are LDS-bound anyway). A 256-thread block is one wave
+// per SIMD, so DGN_DIST_WPE blocks per CU = DGN_DIST_WPE waves per SIMD.
+#ifndef DGN_DIST_WPE
+#define DGN_DIST_WPE 4
+#endif
 template <int CAP>
-__global__ __launch_bounds__(kGraphBlock) void betti_dist_search_kernel(GraphLaunch g, int64_t first, int64_t count,
+__global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void betti_dist_search_kernel(GraphLaunch g, int64_t first, int64_t count,
                                                                          int64_t tri_stride,
                                                                          const int32_t* __restrict__ counts,
                                                                          float* __restrict__ lower,
