@@ -737,8 +737,13 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
         __syncthreads();
         if (chunk0 >= total) break;
         for (int64_t wi = chunk0; wi < chunk0 + kChunk && wi < total; ++wi) {
+#ifdef DGN_UNIFORM_N
+            const int64_t gi = (int64_t)uni((uint32_t)(bl.work_list ? (int64_t)bl.work_list[wi] : wi));
+            const int n = (int)uni((uint32_t)bl.npoints[gi]);
+#else
             const int64_t gi = bl.work_list ? (int64_t)bl.work_list[wi] : wi;
             const int n = bl.npoints[gi];
+#endif
             double* feat = bl.features ? bl.features + 35 * gi : nullptr;
             if (n > NP) {
                 if (bl.skip_above) continue;  // reduced by the overflow launch
@@ -1039,12 +1044,24 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
+#ifdef DGN_HANG_REPRO
+            // diagnostics only (tools/hang_repro.sh): the round-2 form that hung on gfx950 --
+            // the kernel-side forced retry and a `continue` right after the lane-0 append
+            if (bl.force_retry) cx.err |= kErrNA;
+            const uint32_t err = uni(cx.err);
+            if (err && bl.retry_list && (err & kErrCapacity) == err) {
+                if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+                continue;
+            }
+            if (err) {
+#else
             const uint32_t err = uni(cx.err);
             if (err && bl.retry_list && (err & kErrCapacity) == err) {
                 // workspace overflow: the capacity-retry launch (betti_wide_kernel, big layout)
                 // reduces this complex again and writes its outputs
                 if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
             } else if (err) {
+#endif
                 if (lane == 0) atomicOr(bl.error_flag, err);
                 if (feat && lane < 35) feat[lane] = __builtin_nan("");
                 if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
@@ -1147,7 +1164,11 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     const int n = gi < bl.num_atoms ? bl.npoints[gi] : 0;
     const bool mid = gi < bl.num_atoms && n > np_small && n <= 64;
     // above kWideRegular points: straight to the retry list (rank-coded BIG launch)
+#ifdef DGN_HANG_REPRO
+    const bool huge = false;  // diagnostics: the regular wide launch meets them (its skip path)
+#else
     const bool huge = gi < bl.num_atoms && n > kWideRegular && bl.retry_list;
+#endif
     const bool wide = gi < bl.num_atoms && n > 64 && !huge;
     const uint64_t bm = ballot(mid), bw = ballot(wide), bh = ballot(huge);
     if (bh) {

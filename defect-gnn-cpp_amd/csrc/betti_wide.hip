@@ -1083,8 +1083,20 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
         const int64_t wi = q_s;
         __syncthreads();
         if (wi >= total) break;
+#ifdef DGN_UNIFORM_N
+        const int64_t gi = (int64_t)__builtin_amdgcn_readfirstlane(bl.wide_list[wi]);
+        const int n = __builtin_amdgcn_readfirstlane(bl.npoints[gi]);
+#else
         const int64_t gi = (int64_t)bl.wide_list[wi];
         const int n = bl.npoints[gi];
+#endif
+#ifdef DGN_HANG_REPRO
+        // diagnostics only (tools/hang_repro.sh): the round-2 skip that hung on gfx950
+        if (n > ly.nmax && bl.retry_list) {
+            if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+            continue;
+        }
+#endif
         // (no `continue` out of this loop: on gfx950 a uniform continue right after a lane-0
         // atomic was seen to hang the wave; the branches rejoin instead)
         // complexes above kWideRegular points never reach the regular launch (the bucket pass lists
@@ -1190,14 +1202,6 @@ hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves
     if (e != hipSuccess) return e;
     // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges
     return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
-}
-
-bool betti_wide_c16_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("DGN_WIDE_C16");  // A/B: 0 = f32 distances
-        return !(e && e[0] == '0');
-    }();
-    return on;
 }
 
 // waves of betti_wide_kernel resident on the whole device for complexes of up to nmax points

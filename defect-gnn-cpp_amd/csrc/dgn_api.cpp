@@ -84,6 +84,7 @@ struct GraphWork {
     bool have = false;
     bool has_weight = false;  // weight[] holds the 1/count(species) Betti weights of this batch
     const double* pos = nullptr;
+    const int32_t* species = nullptr;  // the species array the weights were computed from
     int64_t atoms = -1, structs = -1;
     double rc = 0, eps = 0;
     uint64_t k = 0;
@@ -122,6 +123,10 @@ struct dgn_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's tables were initialised for
+    // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
+    bool dbg_force_retry = false;  // every complex of a Betti pass through the capacity-retry launch
+    int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
+    bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
     DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
@@ -310,6 +315,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     W.sum_sq = (double)c->host->s.sum_sq;
     W.sum_m = (double)c->host->s.sum_m;
     W.has_weight = want_weight;
+    W.species = b->species;
     if (num_edges) *num_edges = W.edges;
     return DGN_OK;
 }
@@ -417,12 +423,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
         const int64_t resident = betti_wide_resident_waves(
-            c->device, wide_nmax, betti_wide_c16_enabled() && wide_nmax <= kC16MaxPoints);
+            c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
-        if (const char* ev = std::getenv("DGN_WIDE_WAVES")) {  // A/B experiments only
-            const int w = std::atoi(ev);
-            if (w > 0 && w < wide_waves) wide_waves = w;
-        }
+        if (c->dbg_wide_waves > 0 && c->dbg_wide_waves < wide_waves) wide_waves = c->dbg_wide_waves;  // A/B only
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
@@ -460,7 +463,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     HIP_TRY(c, c->b_rlist.ensure(sizeof(int32_t) * (size_t)A));
     bl.retry_list = c->b_rlist.as<int32_t>();
     bl.retry_len = &sc->retry_len;
-    if (const char* fr = std::getenv("DGN_FORCE_RETRY")) bl.force_retry = std::atoi(fr) != 0;  // tests only
+    bl.force_retry = c->dbg_force_retry ? 1 : 0;  // tests only (dgn_ctx_set_debug)
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, c->phase.ensure(32 * sizeof(unsigned long long)));
     HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
@@ -482,7 +485,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
         // the scattered walk and pivot-search reads miss on): the narrow launches and the bucket
         // pass first, then per slice of the wide list its codes (betti_rank_codes) and a wide launch
-        const bool c16 = betti_wide_c16_enabled() && max_points > 64 && max_points <= kC16MaxPoints;
+        const bool c16 = c->dbg_wide_c16 && max_points > 64 && max_points <= kC16MaxPoints;
         {
             TimedLaunch t(c, "betti_vr", bytes, 0.0);
             HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots,
@@ -752,10 +755,24 @@ void dgn_ctx_destroy(dgn_ctx* c) {
 
 int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
     if (!c) return DGN_ERR_ARG;
+    // a graph emit's consistency flag is still being copied on the old stream: let it land before
+    // the stream is swapped, so the next synchronizing call reads it (take_emit_flag syncs only
+    // the current stream)
+    if (c->emit_pending) HIP_TRY(c, hipStreamSynchronize(c->stream));
     // NULL (the legacy null stream, e.g. torch's default stream) -> the context's own blocking
     // stream, which the null stream orders against; anything else is used as given
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
     return DGN_OK;
+}
+
+int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
+    if (!c) return DGN_ERR_ARG;
+    switch (knob) {
+        case DGN_DEBUG_FORCE_RETRY: c->dbg_force_retry = value != 0; return DGN_OK;
+        case DGN_DEBUG_WIDE_WAVES: c->dbg_wide_waves = value > 0 ? value : 0; return DGN_OK;
+        case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
+        default: return fail(c, DGN_ERR_ARG, "dgn_ctx_set_debug: unknown knob " + std::to_string(knob));
+    }
 }
 
 int dgn_ctx_synchronize(dgn_ctx* c) {
@@ -920,7 +937,9 @@ int dgn_dev_graph_betti(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* 
     int st = dgn_dev_graph_emit(c, b, p, row_ptr, o);
     if (st) return st;
     // one neighbour count for both passes when the cutoffs agree (the bench's config: rc 5 / 5)
-    const bool reuse = bp->r_cutoff == p->r_cutoff && p->epsilon == 1e-10 && c->gw.has_weight;
+    // (the 1/count(species) weights are reused only for the species array the count saw)
+    const bool reuse = bp->r_cutoff == p->r_cutoff && p->epsilon == 1e-10 && c->gw.has_weight &&
+                       c->gw.species == b->species;
     return betti_impl(c, b, bp->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0, nullptr, reuse);
 }
 

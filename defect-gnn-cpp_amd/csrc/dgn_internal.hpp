@@ -136,7 +136,6 @@ struct WideLayout {
 WideLayout betti_wide_layout(int nmax, bool big = false);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // device-wide resident waves (occupancy API)
-bool betti_wide_c16_enabled();  // u16 rank codes for wide complexes of <= kC16MaxPoints points (DGN_WIDE_C16=0: off)
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
 // occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
 // equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,

@@ -1654,14 +1654,17 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
         go({0, nt, 0, 0, 0});
         return;
     }
-    static const bool pipeline = [] {
-        const char* e = getenv("DGN_EMIT_PIPELINE");
-        return e && e[0] == '1';
-    }();
-    static const bool split = [] {
-        const char* e = getenv("DGN_EMIT_SPLIT");
-        return e && e[0] == '1';
-    }();
+    // A/B diagnostics builds only (-DDGN_EMIT_PIPELINE / -DDGN_EMIT_SPLIT); never the environment
+#ifdef DGN_EMIT_PIPELINE
+    constexpr bool pipeline = true;
+#else
+    constexpr bool pipeline = false;
+#endif
+#ifdef DGN_EMIT_SPLIT
+    constexpr bool split = true;
+#else
+    constexpr bool split = false;
+#endif
     if (split) {  // diagnostics: all rows, then all RBF (two launches)
         go({0, nt, 0, 0, 0});
         go({0, 0, 0, nt, 0});

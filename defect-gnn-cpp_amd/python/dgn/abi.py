@@ -23,8 +23,9 @@ EXPORTS = [
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
-    "dgn_synth_atoms_per_structure", "dgn_synth_batch",
+    "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug",
 ]
+DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16 = 1, 2, 3
 
 
 class DgnError(RuntimeError):
@@ -96,6 +97,8 @@ def lib():
     L.dgn_ctx_destroy.restype = None
     L.dgn_ctx_set_stream.argtypes = [vp, vp]
     L.dgn_ctx_synchronize.argtypes = [vp]
+    if hasattr(L, "dgn_ctx_set_debug"):  # absent from older A/B builds
+        L.dgn_ctx_set_debug.argtypes = [vp, C.c_int, C.c_int]
     L.dgn_ctx_last_error.restype = C.c_char_p
     L.dgn_ctx_last_error.argtypes = [vp]
     L.dgn_ctx_enable_timing.argtypes = [vp, C.c_int]
@@ -205,6 +208,10 @@ class Context:
 
     def set_stream(self, stream_handle: int | None):
         self._check(lib().dgn_ctx_set_stream(self.h, stream_handle), "set_stream")
+
+    def set_debug(self, knob: int, value: int):
+        """Debug / A-B knob (DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16); tests and tools only."""
+        self._check(lib().dgn_ctx_set_debug(self.h, knob, value), "set_debug")
 
     def synchronize(self):
         self._check(lib().dgn_ctx_synchronize(self.h), "synchronize")

@@ -48,6 +48,13 @@ void dgn_ctx_destroy(dgn_ctx* ctx);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the context's own. */
 int dgn_ctx_set_stream(dgn_ctx* ctx, void* hip_stream);
 int dgn_ctx_synchronize(dgn_ctx* ctx);
+/* Debug / A-B knobs (tests and experiments only; the library never reads the environment):
+ * DGN_DEBUG_FORCE_RETRY  1 = every complex of a Betti pass is reduced again by the capacity-retry
+ *                        launch (the path is then checked on every tier);
+ * DGN_DEBUG_WIDE_WAVES   cap on the wide Betti launch's resident waves (0 = none);
+ * DGN_DEBUG_WIDE_C16     0 = f32 distances for every wide complex (default 1: u16 rank codes). */
+enum { DGN_DEBUG_FORCE_RETRY = 1, DGN_DEBUG_WIDE_WAVES = 2, DGN_DEBUG_WIDE_C16 = 3 };
+int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 const char* dgn_ctx_last_error(const dgn_ctx* ctx);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream around every launch. */
@@ -152,7 +159,9 @@ int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_pa
  * per-atom neighbour counts and hit masks instead of searching a third time: CrystalGraph's
  * NeighborList(rc, K) and compute_structure_betti_features' NeighborList(rc, SIZE_MAX)
  * (betti_features.cpp:107) enumerate the same candidates. The positions must not change between
- * the count and this call (as for dgn_dev_graph_emit). */
+ * the count and this call (as for dgn_dev_graph_emit); the count's 1/count(species) Betti weights are
+ * reused only when `batch->species` is the pointer the count saw, whose contents must not change in
+ * between either (a different pointer: the Betti pass runs its own neighbour count). */
 int dgn_dev_graph_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_graph_params* p, int64_t* row_ptr,
                         const dgn_graph_out* out, const dgn_betti_params* bp, double* features, int32_t* counts);
 

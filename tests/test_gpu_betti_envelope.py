@@ -60,18 +60,20 @@ def test_clique_200_points(ctx):
     print("retry launches:", kt.get("betti_retry", {}).get("launches", 0))
 
 
-def test_forced_capacity_retry_all_tiers(ctx, monkeypatch):
+def test_forced_capacity_retry_all_tiers(ctx):
     """Every complex of a batch spanning the three tiers (<= 48, 49..64, 65..) is routed through
-    the capacity-retry launch (DGN_FORCE_RETRY, a test knob) and still matches Ripser."""
+    the capacity-retry launch (DGN_DEBUG_FORCE_RETRY, a test knob) and still matches Ripser."""
     rng = np.random.default_rng(41)
     sizes = [5, 30, 48, 55, 64, 90, 130]
     clouds = np.zeros((len(sizes), max(sizes), 3))
     for c, n in enumerate(sizes):
         clouds[c, :n] = rng.uniform(0, 5.0, size=(n, 3))
-    monkeypatch.setenv("DGN_FORCE_RETRY", "1")
-    kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
+    ctx.set_debug(dgn.abi.DEBUG_FORCE_RETRY, 1)
+    try:
+        kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_FORCE_RETRY, 0)
     assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
-    monkeypatch.delenv("DGN_FORCE_RETRY")
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
     assert "betti_retry" not in kt
 

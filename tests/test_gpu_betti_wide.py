@@ -79,9 +79,9 @@ def test_f32_instantiations_363_to_512_points(ctx):
     _check_clouds(ctx, clouds, np.array(sizes, dtype=np.int32), 1.7, 8192)
 
 
-def test_f32_fallback_matches_rank_codes(ctx, monkeypatch):
-    """DGN_WIDE_C16=0 (f32 distances for every wide complex) gives the same pairs as the default
-    u16 rank codes; both against verbatim Ripser."""
+def test_f32_fallback_matches_rank_codes(ctx):
+    """DGN_DEBUG_WIDE_C16 = 0 (f32 distances for every wide complex) gives the same pairs as the
+    default u16 rank codes; both against verbatim Ripser."""
     rng = np.random.default_rng(31)
     sizes = [300, 150, 70]
     clouds = np.zeros((len(sizes), max(sizes), 3))
@@ -89,25 +89,14 @@ def test_f32_fallback_matches_rank_codes(ctx, monkeypatch):
         clouds[c, :n] = rng.uniform(0, 6.0, size=(n, 3))
     npts = np.array(sizes, dtype=np.int32)
     _check_clouds(ctx, clouds, npts, 1.9, 8192)
-    monkeypatch.setenv("DGN_WIDE_C16", "0")
-    # the switch is read once per process: run the f32 variant in a child
-    import subprocess
-    import sys
-    import os
-    import tempfile
-    pkg = os.path.dirname(os.path.dirname(os.path.abspath(dgn.__file__)))
-    code = ("import sys; sys.path.insert(0, %r); import numpy as np, dgn; ctx = dgn.Context(0); "
-            "c = np.load(sys.argv[1]); p, k = ctx.host_persistence(c['clouds'], c['npts'], 1.9, cap=8192); "
-            "np.savez(sys.argv[2], p=p, k=k)") % (pkg,)
-    with tempfile.TemporaryDirectory() as td:
-        np.savez(os.path.join(td, "in.npz"), clouds=clouds, npts=npts)
-        r = subprocess.run([sys.executable, "-c", code, os.path.join(td, "in.npz"), os.path.join(td, "out.npz")],
-                           capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0, r.stderr[-2000:]
-        f32 = np.load(os.path.join(td, "out.npz"))
     p16, k16 = ctx.host_persistence(clouds, npts, 1.9, cap=8192)
-    assert np.array_equal(f32["k"], k16)
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_C16, 0)
+    try:
+        p32, k32 = ctx.host_persistence(clouds, npts, 1.9, cap=8192)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_C16, 1)
+    assert np.array_equal(k32, k16)
     for c in range(len(sizes)):  # the emitted pairs (entries past each count are not written)
         for d, col in ((0, 0), (1, 2), (2, 3)):
             n = k16[c, col]
-            assert np.array_equal(f32["p"][c, d, :n], p16[c, d, :n]), (c, d)
+            assert np.array_equal(p32[c, d, :n], p16[c, d, :n]), (c, d)

@@ -11,6 +11,11 @@ import dgn  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 ctx = dgn.Context(0)
+# A/B knobs for this tool only (the library never reads the environment)
+if os.environ.get("DGN_WIDE_WAVES"):
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WAVES, int(os.environ["DGN_WIDE_WAVES"]))
+if os.environ.get("DGN_WIDE_C16"):
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_C16, int(os.environ["DGN_WIDE_C16"]))
 batch = dgn.synth_batch("fcc", 4, B)
 for r in range(reps):
     ctx.reset_timing()
