@@ -8,7 +8,8 @@
 Workload (BASELINE.json configs[3], one shard per GPU, weak scaling): every rank owns B = 8,192
 jittered 256-atom FCC structures (structure ids [rank*B, (rank+1)*B)), inputs resident in HBM.
 One step = the whole hot path over the shard through the C ABI (libdgn.so):
-  graph : NeighborList(rc=5, K=20) + CrystalGraph edge RBF (rc=5, dr=0.1 -> 50 bins, f32)
+  graph : NeighborList(rc=5, K=20) + CrystalGraph edge RBF (rc=5, dr=0.1 -> 50 bins, f64 as the
+          reference's edge_attr, crystal_graph.cpp:30,37; --rbf-dtype f32 for the narrower variant)
   Betti : compute_structure_betti_features(rc=5): NeighborList(rc, inf) + per-atom local VR
           (Gram distances on MFMA, dim 0/1/2, Z/2) + 35 statistics (f64)
 Shards are independent (no collective on the data path); the only collectives are the barrier
@@ -16,10 +17,11 @@ and the max-over-ranks of the timed region.
 Rank 0 prints ONE JSON line (metric/unit from BASELINE.json) with
   roofline      the neighbour + RBF path (prep + count + scan + emit, HBM-bound) at SURVEY 8(d)'s
                 algorithmic bytes over its HIP-event time on the launch stream; the emit launch
-                alone and the f64-RBF variant (measured after the timed loop) beside it
-  side          beside the headline, never part of `value`: BASELINE configs 2, 3 and 5 (1,024 x
-                SC-64 graph / graph + Betti, one 4,096-atom supercell) and the Betti pass at the
-                reference's default 10 A cutoff (32 FCC-256 structures, wide kernel)
+                alone and the f32-RBF variant (measured after the timed loop) beside it
+  side          beside the headline, never part of `value`: BASELINE configs 1, 2, 3 and 5 (the
+                741.vasp POSCAR through the reference CPU path and the GPU path; 1,024 x SC-64 graph
+                / graph + Betti; one 4,096-atom supercell) and the Betti pass at the reference's
+                default 10 A cutoff (32 FCC-256 structures, wide kernel)
   cpu_baseline  the reference CPU path on this host on a bounded sample of the same shard
                 (restated neighbour list + the reference's verbatim vendored Ripser), at the
                 reference's default nesting and at OMP x 1 Ripser thread; its outputs double as the
@@ -55,7 +57,13 @@ def parse():
     ap.add_argument("--dr", type=float, default=0.1)
     ap.add_argument("--betti-rc", type=float, default=5.0)
     ap.add_argument("--no-betti", action="store_true", help="graph only (config 2 style)")
-    ap.add_argument("--no-f64", action="store_true", help="skip the f64-RBF side measurement")
+    ap.add_argument("--rbf-dtype", default="f64", choices=["f64", "f32"],
+                    help="edge_attr dtype of the timed step (the reference's is f64)")
+    ap.add_argument("--no-alt-rbf", action="store_true", help="skip the other-RBF-dtype side measurement")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for the timing barrier / max (nccl = RCCL)")
+    ap.add_argument("--dump-shards", default=None,
+                    help="directory: each rank writes its shard's Betti counts/features and CSR (tests)")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the side lines (BASELINE configs 2/3/5 and the 10 A Betti line)")
     ap.add_argument("--side-reps", type=int, default=3)
@@ -84,11 +92,17 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible devices share them (gloo tests on one GPU)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
+    # the collective's tensors live where the backend expects them
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     import dgn
     from dgn import abi
@@ -100,10 +114,11 @@ def main():
     ctx = dgn.Context(local)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
+    f64 = args.rbf_dtype == "f64"
     gp = abi.graph_params(r_cutoff=args.rc, max_neighbors=args.k, rbf_cutoff=args.rbf_rc, rbf_dr=args.dr,
-                          rbf_dtype=dgn.DGN_F32)
+                          rbf_dtype=dgn.DGN_F64 if f64 else dgn.DGN_F32)
     nbins = abi.lib().dgn_rbf_bins(args.rbf_rc, args.dr)
-    E = sh.alloc_graph(ctx, gp, nbins, torch.float32)
+    E = sh.alloc_graph(ctx, gp, nbins, torch.float64 if f64 else torch.float32)
     if not args.no_betti:
         sh.alloc_betti()
 
@@ -128,7 +143,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ctx.synchronize()  # raises if an emit reported a count/emit disagreement
@@ -151,13 +166,13 @@ def main():
     if all(ktimes.get(k, {}).get("launches") for k in GRAPH_KERNELS):
         path_ms = sum(ktimes[k]["total_ms"] for k in GRAPH_KERNELS) / args.steps
         emit_ms = ktimes["graph_emit"]["total_ms"] / ktimes["graph_emit"]["launches"]
-        algo = graph_bytes_8d(A, B, E, nbins, 4)
+        algo = graph_bytes_8d(A, B, E, nbins, 8 if f64 else 4)
         achieved = algo / (path_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("workload_key") == f"{args.kind}{args.m}x{B}_rc{args.rc}_k{args.k}_nb{nbins}":
+                if tj.get("workload_key") == f"{args.kind}{args.m}x{B}_rc{args.rc}_k{args.k}_nb{nbins}_{args.rbf_dtype}":
                     traffic = tj.get("hbm_bytes_per_path")
             except Exception:
                 traffic = None
@@ -165,12 +180,14 @@ def main():
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": int(algo), "avg_launch_ms": round(path_ms, 4),
-                "bytes_formula": "SURVEY 8(d): 24N+72+4N+8(N+1)+4E+4E(+4E f64 dist)+4*E*n_rbf per structure",
+                "bytes_formula": ("SURVEY 8(d): 24N+72+4N+8(N+1)+4E+4E(+4E f64 dist)+%d*E*n_rbf per structure (%s RBF)"
+                                  % (8 if f64 else 4, args.rbf_dtype)),
                 "emit_only": {"avg_launch_ms": round(emit_ms, 4),
                               "achieved": round(algo / (emit_ms * 1e-3) / 1e9, 1),
                               "frac": round(algo / (emit_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
-        if not args.no_f64:
-            roof["rbf_f64"] = f64_side_measurement(ctx, sh, args, nbins, abi, dgn, torch)
+        if not args.no_alt_rbf:
+            alt = "f32" if f64 else "f64"
+            roof["rbf_" + alt] = alt_rbf_measurement(ctx, sh, args, nbins, abi, dgn, torch, alt)
     dk = ktimes.get("betti_dist", {})
     mfma = None
     if dk.get("launches") and dk["total_ms"] > 0:
@@ -187,9 +204,9 @@ def main():
         "metric": "structures/sec (graph+Betti) at 1/2/4/8 MI355X; HBM GB/s vs peak",
         "value": round(value, 2), "unit": "structures/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f64" if f64 else "f64 (RBF f32)", "data": "synthetic",
         "config": {"workload": (f"{label} shard: {B} x {n_atoms}-atom jittered {args.kind.upper()} per GPU; "
-                                f"graph rc={args.rc} K={args.k} RBF {nbins}xf32"
+                                f"graph rc={args.rc} K={args.k} RBF {nbins}x{args.rbf_dtype}"
                                 + ("" if args.no_betti else f" + Betti-0/1/2 rc={args.betti_rc}")),
                    "structures_per_gpu": B, "atoms_per_structure": n_atoms, "edges_per_gpu": E,
                    "parallelism": f"shard{world}"},
@@ -197,6 +214,8 @@ def main():
         "roofline_mfma": mfma,
         "kernel_ms_per_step": kernel_ms,
     }
+    if args.dump_shards:
+        dump_shard(args.dump_shards, rank, sh, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(args, sh, n_atoms, torch)
     if not args.no_side and world == 1:
@@ -208,25 +227,35 @@ def main():
         dist.destroy_process_group()
 
 
-def f64_side_measurement(ctx, sh, args, nbins, abi, dgn, torch):
-    """The same neighbour path with the reference's f64 edge_attr (crystal_graph.cpp:30,37),
-    measured after the timed loop (HIP events), 3 repetitions."""
-    gp64 = abi.graph_params(r_cutoff=args.rc, max_neighbors=args.k, rbf_cutoff=args.rbf_rc, rbf_dr=args.dr,
-                            rbf_dtype=dgn.DGN_F64)
-    rbf64 = torch.empty((max(sh.E, 1), nbins), dtype=torch.float64, device=sh.dev)
+def dump_shard(d, rank, sh, args):
+    """Tests: this rank's shard outputs (structure ids [rank*B, (rank+1)*B)) as .npy files."""
+    import numpy as np
+    os.makedirs(d, exist_ok=True)
+    for k in ("row_ptr", "col", "dist", "feat", "counts"):
+        if k in sh.out:
+            np.save(os.path.join(d, f"rank{rank}_{k}.npy"), sh.out[k].cpu().numpy())
+
+
+def alt_rbf_measurement(ctx, sh, args, nbins, abi, dgn, torch, alt):
+    """The same neighbour path with the other edge_attr dtype (the reference's is f64,
+    crystal_graph.cpp:30,37), measured after the timed loop (HIP events), 3 repetitions."""
+    f64 = alt == "f64"
+    gpa = abi.graph_params(r_cutoff=args.rc, max_neighbors=args.k, rbf_cutoff=args.rbf_rc, rbf_dr=args.dr,
+                           rbf_dtype=dgn.DGN_F64 if f64 else dgn.DGN_F32)
+    rbfa = torch.empty((max(sh.E, 1), nbins), dtype=torch.float64 if f64 else torch.float32, device=sh.dev)
     reps = 3
     ctx.reset_timing()
     ctx.enable_timing(True)
     for _ in range(reps):
-        ctx.dev_graph_count(sh.batch, gp64)
-        ctx.dev_graph_emit(sh.batch, gp64, sh.out["row_ptr"], sh.out["col"], sh.out["dist"], None, rbf64)
+        ctx.dev_graph_count(sh.batch, gpa)
+        ctx.dev_graph_emit(sh.batch, gpa, sh.out["row_ptr"], sh.out["col"], sh.out["dist"], None, rbfa)
     ctx.synchronize()
     kt = ctx.kernel_times()
     ctx.enable_timing(False)
-    del rbf64
+    del rbfa
     path_ms = sum(kt[k]["total_ms"] for k in GRAPH_KERNELS) / reps
     emit_ms = kt["graph_emit"]["total_ms"] / reps
-    algo = graph_bytes_8d(sh.A, sh.B, sh.E, nbins, 8)
+    algo = graph_bytes_8d(sh.A, sh.B, sh.E, nbins, 8 if f64 else 4)
     return {"algorithmic_bytes_per_launch": int(algo), "avg_launch_ms": round(path_ms, 4),
             "achieved": round(algo / (path_ms * 1e-3) / 1e9, 1),
             "frac": round(algo / (path_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "emit_ms": round(emit_ms, 4)}
@@ -253,6 +282,7 @@ def side_lines(dgn, abi, ctx, dev, args, torch):
         ctx.enable_timing(False)
         return dt, {k: round(v["total_ms"] / args.side_reps, 4) for k, v in kt.items()}
 
+    out["config1"] = config1_line(dgn, abi, ctx, dev, args, torch)
     gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F32)
     nb = abi.lib().dgn_rbf_bins(5.0, 0.1)
     # configs 2 and 3: 1,024 jittered SC-64 cells, graph only / graph + Betti (rc 5)
@@ -289,6 +319,57 @@ def side_lines(dgn, abi, ctx, dev, args, torch):
                          "structures_per_s": round(sh.B / dt, 2), "complexes_per_s": round(sh.A / dt, 1),
                          "ms": round(dt * 1e3, 2), "betti_vr_ms": kt.get("betti_vr")}
     return out
+
+
+def config1_line(dgn, abi, ctx, dev, args, torch):
+    """BASELINE config 1: one POSCAR at 5 A (preprocess_betti.cpp:30-107 on the reference's
+    web/public/data/structures/741.vasp, N = 120, kept as input data in tests/golden/poscar_rc5.npz):
+    NeighborList(5, K = 20) + f64 RBF + compute_structure_betti_features(rc = 5). The GPU path
+    (inputs resident, one dgn_dev_graph_count + dgn_dev_graph_betti per repetition) beside the
+    reference CPU path on this host (restated neighbour list + RBF, verbatim vendored Ripser with
+    OpenMP 8 x 1 Ripser thread), and the GPU outputs checked against the CPU ones."""
+    import numpy as np
+    import oracle_py as O
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "poscar_rc5.npz"))
+    host = {"lattice": fx["741/lattice"][None].copy(), "positions": fx["741/positions"].copy(),
+            "species": fx["741/species"].astype(np.int32),
+            "atom_offset": np.array([0, len(fx["741/positions"])], np.int64)}
+    N = len(host["positions"])
+    batch = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
+    gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F64)
+    nb = abi.lib().dgn_rbf_bins(5.0, 0.1)
+    E = ctx.dev_graph_count(batch, gp)
+    o = {"row_ptr": torch.empty(N + 1, dtype=torch.int64, device=dev), "col": torch.empty(E, dtype=torch.int32, device=dev),
+         "dist": torch.empty(E, dtype=torch.float64, device=dev), "rbf": torch.empty((E, nb), dtype=torch.float64, device=dev),
+         "feat": torch.empty((N, 35), dtype=torch.float64, device=dev), "counts": torch.empty((N, 4), dtype=torch.int32, device=dev)}
+
+    def gpu_step():
+        ctx.dev_graph_count(batch, gp)
+        ctx.dev_graph_betti(batch, gp, o["row_ptr"], o["col"], o["dist"], None, o["rbf"], 5.0, o["feat"], o["counts"])
+
+    gpu_step()
+    torch.cuda.synchronize(dev)
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gpu_step()
+    torch.cuda.synchronize(dev)
+    gpu_s = (time.perf_counter() - t0) / reps
+    line = {"workload": "741.vasp (N = 120): NeighborList(5, 20) + 50-bin f64 RBF + Betti-0/1/2 rc 5",
+            "gpu_ms": round(gpu_s * 1e3, 4), "gpu_structures_per_s": round(1 / gpu_s, 1)}
+    if O.ref_available():
+        t0 = time.perf_counter()
+        O.structure_graph(host["lattice"][0], host["positions"], 5.0, 20, 5.0, 0.1, want_rbf=True)
+        f, c = O.ref_structure_betti(host["lattice"][0], host["positions"], host["species"], 5.0, omp_threads=8,
+                                     ripser_threads=1)
+        cpu_s = time.perf_counter() - t0
+        gf, gc = o["feat"].cpu().numpy(), o["counts"].cpu().numpy()
+        rel = np.abs(gf - f) / np.maximum(np.abs(f), 1e-12)
+        line.update(cpu_ms=round(cpu_s * 1e3, 2), cpu_kind="reference (restated NeighborList + RBF, verbatim Ripser)",
+                    cpu_threads="OpenMP 8 x Ripser 1", cpu_model=cpu_model(), nproc=os.cpu_count(),
+                    counts_exact=bool(np.array_equal(gc, c)))
+        line["feat_within_1e-6"] = bool(np.all((rel <= 1e-6) | (np.abs(gf - f) <= 1e-12)))
+    return line
 
 
 def cpu_model():

@@ -346,34 +346,35 @@ struct Complex {
     uint64_t pk0 = 0, pk1 = 0;
     uint32_t pm0 = 0, pm1 = 0;
 
+    // (branch-free for the register-resident entries: both ballots are taken and the result is
+    // picked with scalar selects, so no uniform branch stalls the wave's instruction fetch)
     __device__ int find_pivot(int npiv, uint64_t tau) const {
         const int lane = lane_id();
-        uint64_t bal = ballot(lane < npiv && pk0 == tau);
-        if (bal) return __ffsll((unsigned long long)bal) - 1;
-        if (npiv > kWave) {
-            bal = ballot(lane + kWave < npiv && pk1 == tau);
-            if (bal) return kWave + __ffsll((unsigned long long)bal) - 1;
-        }
+        const uint64_t b0 = ballot(lane < npiv && pk0 == tau);
+        const uint64_t b1 = ballot(lane + kWave < npiv && pk1 == tau);
+        const int r = b0 ? __ffsll((unsigned long long)b0) - 1 : (b1 ? kWave + __ffsll((unsigned long long)b1) - 1 : -1);
+        if (r >= 0 || npiv <= 2 * kWave) return r;
         const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
         for (int base = 2 * kWave; base < npiv; base += kWave) {
             const int i = base + lane;
-            bal = ballot(i < npiv && sp_piv[i] == tau);
+            const uint64_t bal = ballot(i < npiv && sp_piv[i] == tau);
             if (bal) return base + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
     }
     __device__ uint32_t piv_meta(int i) const {
-        if (i < kWave) return rl(pm0, i);
-        if (i < 2 * kWave) return rl(pm1, i - kWave);
+        const uint32_t m0 = rl(pm0, i & 63), m1 = rl(pm1, i & 63);
+        if (i < 2 * kWave) return i < kWave ? m0 : m1;
         return uni(sp<uint32_t>(ScratchLayout::vmeta)[i]);
     }
     __device__ void piv_push(int i, uint64_t tau, uint32_t meta) {
         const int lane = lane_id();
-        if (i < kWave) {
-            if (lane == i) { pk0 = tau; pm0 = meta; }
-        } else if (i < 2 * kWave) {
-            if (lane == i - kWave) { pk1 = tau; pm1 = meta; }
-        } else if (lane == 0) {
+        const bool s0 = lane == i, s1 = lane + kWave == i;  // entries >= 128 go to scratch
+        pk0 = s0 ? tau : pk0;
+        pm0 = s0 ? meta : pm0;
+        pk1 = s1 ? tau : pk1;
+        pm1 = s1 ? meta : pm1;
+        if (i >= 2 * kWave && lane == 0) {
             sp<uint64_t>(ScratchLayout::piv)[i] = tau;
             sp<uint32_t>(ScratchLayout::vmeta)[i] = meta;
         }
@@ -389,29 +390,24 @@ struct Complex {
     __device__ static uint64_t rl64(uint64_t x, int l) {
         return ((uint64_t)rl((uint32_t)(x >> 32), l) << 32) | rl((uint32_t)x, l);
     }
-    __device__ void v_set(int i, uint32_t sp_) {
+    __device__ void v_set(int i, uint32_t sp_) {  // branch-free: entry i of set 0 or set 1
         const int lane = lane_id();
-        if (i < 64) {
-            if (lane == i) vs0 = sp_;
-        } else if (lane == i - 64) {
-            vs1 = sp_;
-        }
+        vs0 = lane == i ? sp_ : vs0;
+        vs1 = lane + 64 == i ? sp_ : vs1;
     }
     __device__ int v_find(uint32_t x, int v) const {
         const int lane = lane_id();
-        uint64_t bal = ballot(lane < v && vs0 == x);
-        if (bal) return __ffsll((unsigned long long)bal) - 1;
-        if (v > 64) {
-            bal = ballot(lane + 64 < v && vs1 == x);
-            if (bal) return 64 + __ffsll((unsigned long long)bal) - 1;
-        }
-        return -1;
+        const uint64_t b0 = ballot(lane < v && vs0 == x);
+        const uint64_t b1 = ballot(lane + 64 < v && vs1 == x);
+        return b0 ? __ffsll((unsigned long long)b0) - 1 : (b1 ? 64 + __ffsll((unsigned long long)b1) - 1 : -1);
     }
     // V ^= {x} (whole wave, uniform arguments); false on V-list overflow
     __device__ bool v_toggle(int, uint32_t x, int& v) {
         const int pos = v_find(x, v);
         if (pos >= 0) {
-            if (pos != v - 1) v_set(pos, v - 1 < 64 ? rl(vs0, v - 1) : rl(vs1, v - 65));
+            // move the last entry into the hole (both register sets read, the right one picked)
+            const uint32_t l0 = rl(vs0, (v - 1) & 63), l1 = rl(vs1, (v - 65) & 63);
+            v_set(pos, v - 1 < 64 ? l0 : l1);
             v = (int)uni((uint32_t)(v - 1));
             return true;
         }
@@ -466,13 +462,6 @@ struct Complex {
         return ((uint64_t)dd << 32) | (uint64_t)(~pk);
     }
 
-    // lane k's key of the cofacet (V entry e) u {k}, minus base (e wave-uniform)
-    __device__ uint64_t entry_key(int dim, int k, int e, uint64_t base) const {
-        const uint32_t sx = e < 64 ? rl(vs0, e) : rl(vs1, e - 64);
-        const uint32_t dx = e < 64 ? rl(__float_as_uint(vd0), e) : rl(__float_as_uint(vd1), e - 64);
-        return cofacet_key(dim, k, sx, dx) - base;
-    }
-
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
     // multiplicity, restricted to keys above `floor` (the column's previous pivot: adding the
     // owner column cancels it and every other entry of both columns is larger). Lane k
@@ -491,19 +480,25 @@ struct Complex {
             // never kInf)
             const uint64_t base = floor + 1;
             uint64_t lmin = kInf;
-            // kPvUnroll V entries per step, their distance reads in flight together, then the rest
-            int i = 0;
-            for (; i + kPvUnroll <= v; i += kPvUnroll) {
-                uint64_t kq[kPvUnroll];
+            // kPvUnroll V entries per step, their distance reads in flight together, then the rest;
+            // entries 0..63 (register set 0) and 64.. (set 1) in separate loops, so no entry pays a
+            // branch to pick its register set
+            auto scan = [&](uint32_t vs, uint32_t vdb, int cnt) {
+                int i = 0;
+                for (; i + kPvUnroll <= cnt; i += kPvUnroll) {
+                    uint64_t kq[kPvUnroll];
 #pragma unroll
-                for (int u = 0; u < kPvUnroll; ++u) kq[u] = entry_key(dim, k, i + u, base);
+                    for (int u = 0; u < kPvUnroll; ++u) kq[u] = cofacet_key(dim, k, rl(vs, i + u), rl(vdb, i + u)) - base;
 #pragma unroll
-                for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
-            }
-            for (; i < v; ++i) {
-                const uint64_t key = entry_key(dim, k, i, base);
-                lmin = key < lmin ? key : lmin;
-            }
+                    for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
+                }
+                for (; i < cnt; ++i) {
+                    const uint64_t key = cofacet_key(dim, k, rl(vs, i), rl(vdb, i)) - base;
+                    lmin = key < lmin ? key : lmin;
+                }
+            };
+            scan(vs0, __float_as_uint(vd0), v < 64 ? v : 64);
+            if (v > 64) scan(vs1, __float_as_uint(vd1), v - 64);
             const uint64_t mt = wave_min_u64(lmin);
             const uint64_t m = mt + base;
 #ifdef DGN_PHASE_TIMING
@@ -580,19 +575,16 @@ struct Complex {
             uint32_t app0 = kNone;
             bool have_app = false;
             if (regs) {
-                uint64_t bal = ballot(rr0 == ci);
-                if (bal) {
-                    const int l = __ffsll((unsigned long long)bal) - 1;
-                    colkey = rl64(rk0, l);
-                    tau = rl64(rt0, l);
-                    app0 = rl(ra0, l);
-                } else {
-                    bal = ballot(rr1 == ci);
-                    const int l = __ffsll((unsigned long long)bal) - 1;
-                    colkey = rl64(rk1, l);
-                    tau = rl64(rt1, l);
-                    app0 = rl(ra1, l);
-                }
+                // record of rank ci: both register sets read at its lane, the right one picked
+                // (scalar selects, no branch)
+                const uint64_t b0 = ballot(rr0 == ci), b1 = ballot(rr1 == ci);
+                const int l = __ffsll((unsigned long long)(b0 ? b0 : b1)) - 1;
+                const bool in0 = b0 != 0;
+                const uint64_t k0 = rl64(rk0, l), k1 = rl64(rk1, l), t0 = rl64(rt0, l), t1 = rl64(rt1, l);
+                const uint32_t a0 = rl(ra0, l), a1 = rl(ra1, l);
+                colkey = in0 ? k0 : k1;
+                tau = in0 ? t0 : t1;
+                app0 = in0 ? a0 : a1;
                 have_app = true;
             } else {
                 colkey = uni64(sk[ci]);

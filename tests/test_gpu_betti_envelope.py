@@ -37,6 +37,32 @@ def _check(ctx, clouds, npts, thr, cap):
     return kt
 
 
+def _check_lower(ctx, lowers, npts, thr, cap):
+    """host_persistence_lower (compute_persistence_from_distances) on caller-given f32 triangles."""
+    ctx.reset_timing()
+    ctx.enable_timing(True)
+    maxp = int(max(npts))
+    pairs, counts = ctx.host_persistence_lower(lowers, npts, maxp, thr, cap=cap)
+    kt = ctx.kernel_times()
+    ctx.enable_timing(False)
+    bad = []
+    for c in range(len(npts)):
+        n = int(npts[c])
+        r = _ref(lowers[c, :n * (n - 1) // 2], n, np.float32(thr))
+        got = {"dim0": pairs[c, 0, :counts[c, 0]], "dim1": pairs[c, 1, :counts[c, 2]], "dim2": pairs[c, 2, :counts[c, 3]]}
+        ok = all(np.array_equal(np.array(sorted(map(tuple, got[d]))).reshape(-1, 2), r[d].reshape(-1, 2))
+                 for d in got) and counts[c, 1] == r["n_inf0"]
+        if not ok:
+            bad.append((c, n, counts[c].tolist(), [len(r[d]) for d in ("dim0", "dim1", "dim2")], r["n_inf0"]))
+    assert not bad, bad[:8]
+    return kt
+
+
+def _sphere(rng, n):
+    x = rng.standard_normal((n, 3))
+    return x / np.linalg.norm(x, axis=1, keepdims=True)
+
+
 def _cliques(rng, sizes, side=1.0):
     maxp = max(sizes)
     clouds = np.zeros((len(sizes), maxp, 3))
@@ -106,3 +132,36 @@ def test_fcc256_cutoff_12A_above_512_points(ctx):
     fo, co = O.ref_atom_betti(batch["lattice"][0], batch["positions"], batch["species"], 12.0, atoms)
     assert np.array_equal(c[atoms], co), (c[atoms], co)
     np.testing.assert_allclose(f[atoms], fo, rtol=1e-6, atol=1e-12)
+
+
+def test_natural_retry_narrow_clouds(ctx):
+    """Clouds whose reduction outgrows the narrow kernel's caps on its own (no forced retry): points
+    on a unit sphere and on a circle, every pair within the threshold. Their dim-2 (sphere) and
+    dim-1 (circle) columns need long V lists / many non-apparent columns, so the narrow launch
+    appends them to the retry list in the kernel and the big-layout wide launch reduces them;
+    against verbatim Ripser."""
+    rng = np.random.default_rng(53)
+    sizes = [48, 64, 48, 30]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    clouds[0, :48] = _sphere(rng, 48)
+    clouds[1, :64] = _sphere(rng, 64)
+    t = rng.uniform(0, 2 * np.pi, 48)
+    clouds[2, :48] = np.stack([np.cos(t), np.sin(t), 0.01 * rng.standard_normal(48)], 1)
+    clouds[3, :30] = rng.uniform(0, 1.0, size=(30, 3))  # an ordinary complex in the same batch
+    kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 3.0, 1 << 12)
+    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+
+
+def test_natural_retry_narrow_matrices(ctx):
+    """compute_persistence_from_distances on non-Euclidean symmetric matrices (uniform random
+    lengths; lengths from {1, 2, 3, 4}: massive exact ties) of 48 and 64 points: the narrow kernel
+    overflows on its own and the retry launch reduces them; against verbatim Ripser."""
+    rng = np.random.default_rng(59)
+    sizes = [48, 48, 64]
+    maxp = max(sizes)
+    lowers = np.zeros((len(sizes), maxp * (maxp - 1) // 2), np.float32)
+    for c, (n, kind) in enumerate(zip(sizes, ("uniform", "ties4", "uniform"))):
+        M = rng.uniform(0.0, 1.0, (n, n)) if kind == "uniform" else rng.integers(1, 5, (n, n)).astype(np.float64)
+        lowers[c, :n * (n - 1) // 2] = np.array([M[i, j] for i in range(1, n) for j in range(i)], np.float32)
+    kt = _check_lower(ctx, lowers, np.array(sizes, dtype=np.int32), 5.0, 1 << 12)
+    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt

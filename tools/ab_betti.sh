@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 for arm in A B A B; do
   lib=$A; [ $arm = B ] && lib=$B
-  DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-f64 > "$OUT/bench_$arm.json" 2>> "$OUT/err.log"
+  DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-alt-rbf > "$OUT/bench_$arm.json" 2>> "$OUT/err.log"
   python -c "import json,sys; r=json.load(open('$OUT/bench_$arm.json')); print('$arm', r['value'], r['kernel_ms_per_step']['betti_vr'])"
 done
 if [ -n "$DA" ]; then

@@ -8,7 +8,7 @@ mkdir -p "$OUT"
 for r in 1 2; do
   for lib in "$@"; do
     name=$(basename "$lib" .so)
-    DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-betti --no-f64 $BENCH_ARGS \
+    DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-betti --no-alt-rbf $BENCH_ARGS \
         > "$OUT/${name}_$r.json" 2>> "$OUT/err.log"
     python -c "import json; r=json.load(open('$OUT/${name}_$r.json')); k=r['kernel_ms_per_step']; print('$name', {n: k[n] for n in k if not n.startswith('betti')})"
   done

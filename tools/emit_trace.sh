@@ -6,7 +6,7 @@ OUT=$1; LIB=$2
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 DGN_LIB=$LIB timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-betti --no-f64 > "$OUT/b.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-betti --no-alt-rbf > "$OUT/b.log" 2>&1
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
 f = sorted(glob.glob(sys.argv[1] + "/tr/**/*kernel_trace.csv", recursive=True))[-1]

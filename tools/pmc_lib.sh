@@ -11,6 +11,6 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_INSTS_VALU_CVT"; do
   i=$((i+1))
   DGN_LIB=$LIB timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-side --no-betti --no-f64 > "$OUT/p$i.log" 2>&1
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-side --no-betti --no-alt-rbf > "$OUT/p$i.log" 2>&1
 done
 python3 tools/pmc_summary.py "$OUT" count emit > "$OUT/summary.txt"
