@@ -4,7 +4,8 @@ ARCH     ?= gfx950
 PKG      := defect-gnn-cpp_amd
 CSRC     := $(PKG)/csrc
 BUILD    := $(PKG)/build
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I$(CSRC) -Iinclude
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result -I$(CSRC) -Iinclude \
+            -mllvm -amdgpu-atomic-optimizer-strategy=DPP
 LIB      := $(PKG)/lib/libdgn.so
 
 KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/betti_rank.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o

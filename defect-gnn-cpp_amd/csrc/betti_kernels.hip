@@ -64,6 +64,7 @@ constexpr uint32_t kErrPiv = 1u << 3;
 constexpr uint32_t kErrPairs = 1u << 4;
 constexpr uint32_t kErrR = 1u << 5;
 [[maybe_unused]] constexpr uint32_t kErrOrder = 1u << 6;  // -DDGN_ORDER_CHECK builds
+[[maybe_unused]] constexpr uint32_t kErrExec = 1u << 8;   // -DDGN_EXEC_CHECK builds
 constexpr uint32_t kErrCapacity = kErrWorkCol | kErrNA | kErrPiv | kErrPairs | kErrR;
 
 // scratch layout per wave (bytes)
@@ -346,35 +347,34 @@ struct Complex {
     uint64_t pk0 = 0, pk1 = 0;
     uint32_t pm0 = 0, pm1 = 0;
 
-    // (branch-free for the register-resident entries: both ballots are taken and the result is
-    // picked with scalar selects, so no uniform branch stalls the wave's instruction fetch)
     __device__ int find_pivot(int npiv, uint64_t tau) const {
         const int lane = lane_id();
-        const uint64_t b0 = ballot(lane < npiv && pk0 == tau);
-        const uint64_t b1 = ballot(lane + kWave < npiv && pk1 == tau);
-        const int r = b0 ? __ffsll((unsigned long long)b0) - 1 : (b1 ? kWave + __ffsll((unsigned long long)b1) - 1 : -1);
-        if (r >= 0 || npiv <= 2 * kWave) return r;
+        uint64_t bal = ballot(lane < npiv && pk0 == tau);
+        if (bal) return __ffsll((unsigned long long)bal) - 1;
+        if (npiv > kWave) {
+            bal = ballot(lane + kWave < npiv && pk1 == tau);
+            if (bal) return kWave + __ffsll((unsigned long long)bal) - 1;
+        }
         const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
         for (int base = 2 * kWave; base < npiv; base += kWave) {
             const int i = base + lane;
-            const uint64_t bal = ballot(i < npiv && sp_piv[i] == tau);
+            bal = ballot(i < npiv && sp_piv[i] == tau);
             if (bal) return base + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
     }
     __device__ uint32_t piv_meta(int i) const {
-        const uint32_t m0 = rl(pm0, i & 63), m1 = rl(pm1, i & 63);
-        if (i < 2 * kWave) return i < kWave ? m0 : m1;
+        if (i < kWave) return rl(pm0, i);
+        if (i < 2 * kWave) return rl(pm1, i - kWave);
         return uni(sp<uint32_t>(ScratchLayout::vmeta)[i]);
     }
     __device__ void piv_push(int i, uint64_t tau, uint32_t meta) {
         const int lane = lane_id();
-        const bool s0 = lane == i, s1 = lane + kWave == i;  // entries >= 128 go to scratch
-        pk0 = s0 ? tau : pk0;
-        pm0 = s0 ? meta : pm0;
-        pk1 = s1 ? tau : pk1;
-        pm1 = s1 ? meta : pm1;
-        if (i >= 2 * kWave && lane == 0) {
+        if (i < kWave) {
+            if (lane == i) { pk0 = tau; pm0 = meta; }
+        } else if (i < 2 * kWave) {
+            if (lane == i - kWave) { pk1 = tau; pm1 = meta; }
+        } else if (lane == 0) {
             sp<uint64_t>(ScratchLayout::piv)[i] = tau;
             sp<uint32_t>(ScratchLayout::vmeta)[i] = meta;
         }
@@ -390,24 +390,29 @@ struct Complex {
     __device__ static uint64_t rl64(uint64_t x, int l) {
         return ((uint64_t)rl((uint32_t)(x >> 32), l) << 32) | rl((uint32_t)x, l);
     }
-    __device__ void v_set(int i, uint32_t sp_) {  // branch-free: entry i of set 0 or set 1
+    __device__ void v_set(int i, uint32_t sp_) {
         const int lane = lane_id();
-        vs0 = lane == i ? sp_ : vs0;
-        vs1 = lane + 64 == i ? sp_ : vs1;
+        if (i < 64) {
+            if (lane == i) vs0 = sp_;
+        } else if (lane == i - 64) {
+            vs1 = sp_;
+        }
     }
     __device__ int v_find(uint32_t x, int v) const {
         const int lane = lane_id();
-        const uint64_t b0 = ballot(lane < v && vs0 == x);
-        const uint64_t b1 = ballot(lane + 64 < v && vs1 == x);
-        return b0 ? __ffsll((unsigned long long)b0) - 1 : (b1 ? 64 + __ffsll((unsigned long long)b1) - 1 : -1);
+        uint64_t bal = ballot(lane < v && vs0 == x);
+        if (bal) return __ffsll((unsigned long long)bal) - 1;
+        if (v > 64) {
+            bal = ballot(lane + 64 < v && vs1 == x);
+            if (bal) return 64 + __ffsll((unsigned long long)bal) - 1;
+        }
+        return -1;
     }
     // V ^= {x} (whole wave, uniform arguments); false on V-list overflow
     __device__ bool v_toggle(int, uint32_t x, int& v) {
         const int pos = v_find(x, v);
         if (pos >= 0) {
-            // move the last entry into the hole (both register sets read, the right one picked)
-            const uint32_t l0 = rl(vs0, (v - 1) & 63), l1 = rl(vs1, (v - 65) & 63);
-            v_set(pos, v - 1 < 64 ? l0 : l1);
+            if (pos != v - 1) v_set(pos, v - 1 < 64 ? rl(vs0, v - 1) : rl(vs1, v - 65));
             v = (int)uni((uint32_t)(v - 1));
             return true;
         }
@@ -482,7 +487,8 @@ struct Complex {
             uint64_t lmin = kInf;
             // kPvUnroll V entries per step, their distance reads in flight together, then the rest;
             // entries 0..63 (register set 0) and 64.. (set 1) in separate loops, so no entry pays a
-            // branch to pick its register set
+            // branch to pick its register set (A/B: 196.0 -> 189.4 ms per shard; making the pivot
+            // table, V-list and column-record selects branch-free as well cost +2 %)
             auto scan = [&](uint32_t vs, uint32_t vdb, int cnt) {
                 int i = 0;
                 for (; i + kPvUnroll <= cnt; i += kPvUnroll) {
@@ -575,16 +581,19 @@ struct Complex {
             uint32_t app0 = kNone;
             bool have_app = false;
             if (regs) {
-                // record of rank ci: both register sets read at its lane, the right one picked
-                // (scalar selects, no branch)
-                const uint64_t b0 = ballot(rr0 == ci), b1 = ballot(rr1 == ci);
-                const int l = __ffsll((unsigned long long)(b0 ? b0 : b1)) - 1;
-                const bool in0 = b0 != 0;
-                const uint64_t k0 = rl64(rk0, l), k1 = rl64(rk1, l), t0 = rl64(rt0, l), t1 = rl64(rt1, l);
-                const uint32_t a0 = rl(ra0, l), a1 = rl(ra1, l);
-                colkey = in0 ? k0 : k1;
-                tau = in0 ? t0 : t1;
-                app0 = in0 ? a0 : a1;
+                uint64_t bal = ballot(rr0 == ci);
+                if (bal) {
+                    const int l = __ffsll((unsigned long long)bal) - 1;
+                    colkey = rl64(rk0, l);
+                    tau = rl64(rt0, l);
+                    app0 = rl(ra0, l);
+                } else {
+                    bal = ballot(rr1 == ci);
+                    const int l = __ffsll((unsigned long long)bal) - 1;
+                    colkey = rl64(rk1, l);
+                    tau = rl64(rt1, l);
+                    app0 = rl(ra1, l);
+                }
                 have_app = true;
             } else {
                 colkey = uni64(sk[ci]);
@@ -707,7 +716,6 @@ struct Complex {
 template <int NP>
 __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
-    __shared__ int64_t chunk_s;
 #ifdef DGN_PHASE_TIMING
     // diagnostics counters in LDS (registers would change the kernel's occupancy)
     __shared__ uint64_t ph[32];
@@ -723,19 +731,34 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
     // complexes of this launch: all of them, or the overflow list written by the bucket pass
     const int64_t total = bl.work_list ? (int64_t)*bl.overflow_len : A;
     for (;;) {
-        if (lane == 0) chunk_s = (int64_t)atomicAdd((unsigned int*)bl.queue, 1u) * kChunk;
-        __syncthreads();
-        const int64_t chunk0 = chunk_s;
-        __syncthreads();
+#ifdef DGN_EXEC_CHECK
+        // diagnostics: every lane must be live at the dequeue
+        {
+            const uint64_t ex = __builtin_amdgcn_read_exec();
+            if (ex != ~0ull) {
+                if (lane == __ffsll((unsigned long long)ex) - 1) {
+                    atomicOr(bl.error_flag, kErrExec);
+                    printf("DGN_EXEC_CHECK: exec %016lx at the dequeue (block %d)\n", (unsigned long)ex, (int)blockIdx.x);
+                }
+                return;
+            }
+        }
+#endif
+        // Wave-uniform dequeue without a branch on the lane: every lane adds (lane == 0) to the
+        // queue (one atomic after the compiler's wave combine) and lane 0's ticket is read back
+        // with v_readlane into an SGPR, so the loop exit and everything keyed on the complex (gi,
+        // n) are scalar branches. Round 2 handed lane 0's ticket to the wave through an LDS slot
+        // behind `if (lane == 0)`; a `continue` out of the loop then let the compiler thread a copy
+        // of the loop head specialised for lanes 1..63 -- for them the atomic is skipped, so the
+        // copy re-reads the unchanged slot (a `readlane` of the specialised ticket constant-folds
+        // to the same effect) and spins while lane 0 waits in the exit guard: the gfx950 "hang"
+        // (DESIGN.md 3.2).
+        const uint32_t ticket = atomicAdd((unsigned int*)bl.queue, lane == 0 ? 1u : 0u);
+        const int64_t chunk0 = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)ticket, 0) * kChunk;
         if (chunk0 >= total) break;
         for (int64_t wi = chunk0; wi < chunk0 + kChunk && wi < total; ++wi) {
-#ifdef DGN_UNIFORM_N
-            const int64_t gi = (int64_t)uni((uint32_t)(bl.work_list ? (int64_t)bl.work_list[wi] : wi));
+            const int64_t gi = bl.work_list ? (int64_t)(int32_t)uni((uint32_t)bl.work_list[wi]) : wi;
             const int n = (int)uni((uint32_t)bl.npoints[gi]);
-#else
-            const int64_t gi = bl.work_list ? (int64_t)bl.work_list[wi] : wi;
-            const int n = bl.npoints[gi];
-#endif
             double* feat = bl.features ? bl.features + 35 * gi : nullptr;
             if (n > NP) {
                 if (bl.skip_above) continue;  // reduced by the overflow launch
@@ -1037,8 +1060,9 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
 #ifdef DGN_HANG_REPRO
-            // diagnostics only (tools/hang_repro.sh): the round-2 form that hung on gfx950 --
-            // the kernel-side forced retry and a `continue` right after the lane-0 append
+            // diagnostics only (tools/hang_repro.sh): the round-2 form that hung with the LDS-slot
+            // dequeue (the kernel-side forced retry and a `continue` right after the lane-0
+            // append); with the uniform dequeue it is an ordinary scalar branch
             if (bl.force_retry) cx.err |= kErrNA;
             const uint32_t err = uni(cx.err);
             if (err && bl.retry_list && (err & kErrCapacity) == err) {

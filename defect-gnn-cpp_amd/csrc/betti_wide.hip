@@ -109,6 +109,9 @@ struct WideCx {
     uint32_t err;
     int n_d0, n_inf0, n_p1, n_p2;
     const uint32_t* vals = nullptr;  // CODED: the complex's sorted f32 distances (code -> value)
+#ifdef DGN_PHASE_TIMING
+    uint64_t dg_searches = 0, dg_floor_iters = 0;  // diagnostics: pivot searches and their floor rounds
+#endif
 
     __device__ float value(uint32_t dc) const { return CODED ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
 
@@ -778,7 +781,13 @@ struct WideCx {
         // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
         const uint32_t vl0 = k < v ? VL[k] : 0u;
         const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
+#ifdef DGN_PHASE_TIMING
+        ++dg_searches;
+#endif
         for (;;) {
+#ifdef DGN_PHASE_TIMING
+            ++dg_floor_iters;
+#endif
             uint64_t lmin = kInfW, lp = 0;
             int lcnt = 0;
             auto eval = [&](uint32_t s, uint32_t ds) {
@@ -967,6 +976,9 @@ struct WideCx {
             for (int k = 0; k < 6; ++k) atomicAdd(&bl.phase_cycles[16 + k], (unsigned long long)sb[k]);
             atomicAdd(&bl.phase_cycles[24], (unsigned long long)sb[6]);
             atomicAdd(&bl.phase_cycles[25], (unsigned long long)sb[7]);
+            atomicAdd(&bl.phase_cycles[29], (unsigned long long)dg_searches);
+            atomicAdd(&bl.phase_cycles[30], (unsigned long long)dg_floor_iters);
+            dg_searches = dg_floor_iters = 0;
         }
 #endif
 #undef WSUB
@@ -1068,37 +1080,30 @@ struct WideCx {
 template <int KW, int MODE>
 __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const WideLayout& ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
-    // [nmax] u16, the dequeue slot
+    // [nmax] u16
     extern __shared__ uint64_t wide_lds[];
     const int64_t ww = (ly.nmax + 63) / 64;
     uint64_t* adj = wide_lds;
     uint16_t* par = reinterpret_cast<uint16_t*>(wide_lds + ly.nmax * ww);
-    int64_t& q_s = *reinterpret_cast<int64_t*>(wide_lds + ly.nmax * ww + (ly.nmax + 3) / 4);
     const int lane = lane_id();
     uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
     const int64_t total = (int64_t)*bl.wide_len;
     for (;;) {
-        if (lane == 0) q_s = (int64_t)atomicAdd(bl.wide_queue, 1u);
-        __syncthreads();
-        const int64_t wi = q_s;
-        __syncthreads();
+        // wave-uniform dequeue without a branch on the lane (see betti_kernels.hip): every lane adds
+        // (lane == 0), lane 0's ticket goes to an SGPR
+        const uint32_t ticket = atomicAdd(bl.wide_queue, lane == 0 ? 1u : 0u);
+        const int64_t wi = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)ticket, 0);
         if (wi >= total) break;
-#ifdef DGN_UNIFORM_N
-        const int64_t gi = (int64_t)__builtin_amdgcn_readfirstlane(bl.wide_list[wi]);
-        const int n = __builtin_amdgcn_readfirstlane(bl.npoints[gi]);
-#else
-        const int64_t gi = (int64_t)bl.wide_list[wi];
-        const int n = bl.npoints[gi];
-#endif
+        const int64_t gi = (int64_t)(int32_t)uniw((uint32_t)bl.wide_list[wi]);
+        const int n = (int)uniw((uint32_t)bl.npoints[gi]);
 #ifdef DGN_HANG_REPRO
-        // diagnostics only (tools/hang_repro.sh): the round-2 skip that hung on gfx950
+        // diagnostics only (tools/hang_repro.sh): the round-2 skip that hung with the LDS-slot
+        // dequeue; with the uniform dequeue above it is an ordinary scalar branch
         if (n > ly.nmax && bl.retry_list) {
             if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
             continue;
         }
 #endif
-        // (no `continue` out of this loop: on gfx950 a uniform continue right after a lane-0
-        // atomic was seen to hang the wave; the branches rejoin instead)
         // complexes above kWideRegular points never reach the regular launch (the bucket pass lists
         // them for the rank-coded retry launch); a larger one here is outside the layout
         if (n > ly.nmax) {
@@ -1148,7 +1153,7 @@ WideKernel wide_kernel_for(int nmax, bool c16) {
 
 size_t wide_lds_bytes(int nmax) {
     const int64_t ww = (nmax + 63) / 64;
-    return (size_t)(8 * (nmax * ww + (nmax + 3) / 4 + 1));
+    return (size_t)(8 * (nmax * ww + (nmax + 3) / 4));
 }
 
 }  // namespace
@@ -1156,12 +1161,20 @@ size_t wide_lds_bytes(int nmax) {
 // Scratch layout of one wave for complexes of up to nmax points (all offsets 256-B aligned).
 // big = the capacity-retry layout (complexes whose reduction outgrew the regular caps): column,
 // pivot and pair tables sized for every simplex of the complex, a 16M-entry V store.
-WideLayout betti_wide_layout(int nmax, bool big) {
+WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit) {
     WideLayout l{};
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
     int64_t cap = 1024;
-    const int64_t cap_max = big ? (int64_t(1) << 24) : (int64_t(1) << 17);
+    // the big (capacity-retry) layout caps its column / pivot / pair tables at 2^24 entries and its
+    // V store at 2^24 words: a complex that outgrows even these (e.g. a dense clique of several
+    // hundred points, C(n, 3) > 2^24 above ~465 points) fails with DGN_ERR_CAPACITY
+    int64_t cap_max = big ? (int64_t(1) << 24) : (int64_t(1) << 17);
+    if (!big && cap_limit > 0) {
+        cap_max = 64;
+        while (cap_max < cap_limit) cap_max <<= 1;
+        cap = cap_max < cap ? cap_max : cap;
+    }
     while ((cap < t || cap < e) && cap < cap_max) cap <<= 1;
     l.nmax = nmax;
     l.na_cap = (int32_t)cap;

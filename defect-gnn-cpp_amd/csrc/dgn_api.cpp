@@ -122,10 +122,11 @@ struct dgn_ctx {
     // overflow-tier fork (side stream + events), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int wide_nmax = 0, wide_waves = 0;  // layout the wide scratch's tables were initialised for
+    int wide_nmax = 0, wide_waves = 0, wide_cap = 0;  // layout the wide scratch's tables were initialised for
     // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
     bool dbg_force_retry = false;  // every complex of a Betti pass through the capacity-retry launch
     int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
+    int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
@@ -415,7 +416,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     int wide_waves = 0;
     if (max_points > 64) {
         const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
-        wl = betti_wide_layout(wide_nmax);
+        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap);
         // as many waves as the device keeps resident (dynamic LDS sized by max_points), each
         // with its own scratch, within half of the free HBM (288 GB per MI355X; at least 8 GB)
         size_t free_b = 0, total_b = 0;
@@ -430,13 +431,14 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
-        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves) {
+        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap) {
             // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
             // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
             // restores both for the entries it used
             HIP_TRY(c, betti_wide_init_scratch(c->stream, wl, wide_waves));
             c->wide_nmax = wide_nmax;
             c->wide_waves = wide_waves;
+            c->wide_cap = wl.na_cap;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
@@ -662,6 +664,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     const uint32_t f = c->host->s.error_flag;
     if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
     if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
+    if (f & 256u) return fail(c, DGN_ERR_INTERNAL, "partial EXEC mask at a Betti dequeue (DGN_EXEC_CHECK build)");
     if (f) return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
     return DGN_OK;
 }
@@ -771,6 +774,7 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
         case DGN_DEBUG_FORCE_RETRY: c->dbg_force_retry = value != 0; return DGN_OK;
         case DGN_DEBUG_WIDE_WAVES: c->dbg_wide_waves = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
+        case DGN_DEBUG_WIDE_CAP: c->dbg_wide_cap = value > 0 ? value : 0; return DGN_OK;
         default: return fail(c, DGN_ERR_ARG, "dgn_ctx_set_debug: unknown knob " + std::to_string(knob));
     }
 }

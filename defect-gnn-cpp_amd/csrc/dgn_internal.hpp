@@ -133,7 +133,10 @@ struct WideLayout {
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
     int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2, d0;
 };
-WideLayout betti_wide_layout(int nmax, bool big = false);
+// cap_limit > 0 (tests, DGN_DEBUG_WIDE_CAP): the regular layout's column / pivot / pair tables
+// hold at most cap_limit entries, so ordinary complexes overflow in the kernel and take the
+// capacity-retry path
+WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // device-wide resident waves (occupancy API)
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first

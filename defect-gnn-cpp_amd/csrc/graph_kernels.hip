@@ -1139,6 +1139,56 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
     }
 }
 
+// The tile's RBF block as flat 16-byte units, one per thread per step (all kGraphBlock threads,
+// consecutive threads -> consecutive units): element f of the block is (edge f / nb, bin f % nb);
+// d[] (LDS) holds the block's distances with one slack entry past the last edge.
+template <typename T>
+__device__ __forceinline__ void rbf_direct(T* __restrict__ out, int total, const DGN_LDS double* d, const RbfSpec& rs) {
+    constexpr int V = 16 / sizeof(T);
+    const int nb = rs.nbins;
+    const int mis = (int)(((uintptr_t)out / sizeof(T)) & (V - 1));
+    int head = mis ? V - mis : 0;
+    head = head < total ? head : total;
+    auto one = [&](int f) -> T {
+        int e, k;
+        rbf_split(f, rs, e, k);
+        const double t = (double)k * rs.dr - d[e];
+        if constexpr (sizeof(T) == 4) return rbf_f32(t, rs);
+        else return rs.norm * exp_bounded<12>(-0.5 * (t * t) * rs.inv_sigma2);
+    };
+    const int tix = threadIdx.x;
+    if (tix < head) out[tix] = one(tix);
+    const int nvec = (total - head) / V;
+    typedef T vec_t __attribute__((ext_vector_type(V)));
+    for (int v = tix; v < nvec; v += kGraphBlock) {
+        const int f = head + V * v;
+        int e, k;
+        rbf_split(f, rs, e, k);
+        double de = d[e];
+        double t = (double)k * rs.dr - de;
+        vec_t o;
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            // f64: t = k dr - d afresh per value (edge_features.cpp:20-21); f32: t steps by dr
+            if constexpr (sizeof(T) == 4) o[u] = rbf_f32(t, rs);
+            else o[u] = rs.norm * exp_bounded<12>(-0.5 * (t * t) * rs.inv_sigma2);
+            if (++k == nb) {
+                k = 0;
+                de = d[++e];  // d has one slack entry past the last edge
+            }
+            if constexpr (sizeof(T) == 4) t = k ? t + rs.dr : -de;
+            else t = (double)k * rs.dr - de;
+        }
+#ifdef DGN_RBF_PLAIN_STORE
+        *reinterpret_cast<vec_t*>(out + f) = o;
+#else
+        __builtin_nontemporal_store(o, reinterpret_cast<vec_t*>(out + f));
+#endif
+    }
+    const int t0 = head + V * nvec;
+    if (t0 + tix < total) out[t0 + tix] = one(t0 + tix);
+}
+
 // ------------------------------------------------------------------------------------------
 // Kernel 3: fused emit. Per atom (one wave): compact the hits (the count pass's mask, or a search)
 // into LDS, rank, write the kept rows (col, distance, displacement). STREAM (max_neighbors <=
@@ -1262,6 +1312,16 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             for (int i = threadIdx.x; i < ne; i += kGraphBlock) dl[i] = dist[e0 + i];
             __syncthreads();
         }
+#ifdef DGN_RBF_DIRECT
+        // A/B: every 16-byte unit computed straight into registers (no LDS staging): f32 with
+        // v_exp_f32 per value, f64 with the bounded Taylor exp per value
+        if (rs.dtype == 1)
+            rbf_direct(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne * rs.nbins, dl, rs);
+        else
+            rbf_direct(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne * rs.nbins, dl, rs);
+        EMIT_STAMP(4);
+        return;
+#endif
         if (rs.dtype == 1)
             rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
                             reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);

@@ -25,7 +25,7 @@ EXPORTS = [
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug",
 ]
-DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16 = 1, 2, 3
+DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP = 1, 2, 3, 4
 
 
 class DgnError(RuntimeError):

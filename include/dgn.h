@@ -52,8 +52,11 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  * DGN_DEBUG_FORCE_RETRY  1 = every complex of a Betti pass is reduced again by the capacity-retry
  *                        launch (the path is then checked on every tier);
  * DGN_DEBUG_WIDE_WAVES   cap on the wide Betti launch's resident waves (0 = none);
- * DGN_DEBUG_WIDE_C16     0 = f32 distances for every wide complex (default 1: u16 rank codes). */
-enum { DGN_DEBUG_FORCE_RETRY = 1, DGN_DEBUG_WIDE_WAVES = 2, DGN_DEBUG_WIDE_C16 = 3 };
+ * DGN_DEBUG_WIDE_C16     0 = f32 distances for every wide complex (default 1: u16 rank codes);
+ * DGN_DEBUG_WIDE_CAP     > 0: the wide launch's column / pivot / pair tables hold at most this many
+ *                        entries (rounded up to a power of two), so ordinary complexes overflow in the
+ *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps. */
+enum { DGN_DEBUG_FORCE_RETRY = 1, DGN_DEBUG_WIDE_WAVES = 2, DGN_DEBUG_WIDE_C16 = 3, DGN_DEBUG_WIDE_CAP = 4 };
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 const char* dgn_ctx_last_error(const dgn_ctx* ctx);
 

@@ -6,7 +6,7 @@ TAG=$1; FLAGS=${2:-}
 cd "$(dirname "$0")/.."
 B=defect-gnn-cpp_amd/build_var_$TAG
 mkdir -p "$B"
-HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Idefect-gnn-cpp_amd/csrc -Iinclude $FLAGS"
+HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Idefect-gnn-cpp_amd/csrc -Iinclude -mllvm -amdgpu-atomic-optimizer-strategy=DPP $FLAGS"
 for f in graph_kernels betti_kernels betti_wide betti_rank node_kernels; do
   /opt/rocm/bin/hipcc $HF -c defect-gnn-cpp_amd/csrc/$f.hip -o $B/$f.o &
 done

@@ -31,4 +31,5 @@ print(json.dumps({"complexes": A, "s": round(dt, 3), "cycles_per_complex": round
                   "adds_per_complex": ph[24] / A,
                   "dim2_walk": {"columns_walked": ph[28] / A, "mean_steps": ph[26] / max(ph[28], 1),
                                 "wave_iterations_per_complex": ph[27] / A,
-                                "lane_efficiency": ph[26] / max(64 * ph[27], 1)}, "mean_V_per_pivot_search": ph[25] / max(ph[24], 1)}, indent=1))
+                                "lane_efficiency": ph[26] / max(64 * ph[27], 1)}, "mean_V_per_pivot_search": ph[25] / max(ph[24], 1),
+                  "pivot_searches_per_complex": ph[29] / A, "floor_rounds_per_search": ph[30] / max(ph[29], 1)}, indent=1))
