@@ -1114,6 +1114,7 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
             WideCx<KW, MODE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
             if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
             cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
+            if (bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
         }
     }
 }

@@ -99,7 +99,14 @@ struct HostScalars {
     Scalars s;
     uint32_t emit_flag;  // copied asynchronously after every graph emit
     uint32_t pad;
+    uint32_t betti_flags[2];  // copied asynchronously after every Betti pass: search, reduction bits
 };
+
+// sticky device words of the Betti pass (context lifetime; never cleared by a count pass): the
+// Betti search's consistency bits, the reduction's error bits, and the number of complexes the
+// capacity-retry launches reduced. A pass ORs into the first two; take_betti_flag clears them once
+// the host has read them.
+enum { kBFSearch = 0, kBFReduce = 1, kBFRetried = 2, kBFWords = 4 };
 
 }  // namespace
 
@@ -115,6 +122,9 @@ struct dgn_ctx {
     DevBuf scalars;
     HostScalars* host = nullptr;  // pinned
     bool emit_pending = false;    // an emit's error flag is on its way to host->emit_flag
+    bool betti_pending = false;   // a Betti pass's flags are on their way to host->betti_flags
+    DevBuf bflags;                // [kBFWords] sticky Betti words (above)
+    int big_nmax = 0, big_waves = 0;  // capacity-retry workspace (b_big) the tables were initialised for
     // betti workspace
     DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big, b_rank, b_rscal, b_rank16, b_rscal16;
     int betti_slots = 0;
@@ -239,6 +249,32 @@ int take_emit_flag(dgn_ctx* c) {
     return fail(c, DGN_ERR_INTERNAL, "graph emit disagreed with the count pass (flags " + std::to_string(f) + ")" + why);
 }
 
+// A Betti pass reports its flags asynchronously (host->betti_flags, copied at the end of the pass on
+// its stream); the next call that synchronizes the stream surfaces them, and clears the sticky
+// device words it reported.
+int take_betti_flag(dgn_ctx* c) {
+    if (!c->betti_pending) return DGN_OK;
+    c->betti_pending = false;
+    const uint32_t g = c->host->betti_flags[kBFSearch], f = c->host->betti_flags[kBFReduce];
+    if (!g && !f) return DGN_OK;
+    HIP_TRY(c, hipMemsetAsync(c->bflags.p, 0, 2 * sizeof(uint32_t), c->stream));
+    if (g)
+        return fail(c, DGN_ERR_INTERNAL, "Betti neighbour search disagreed with the count pass (flags " + std::to_string(g) + ")");
+    if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
+    if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
+    if (f & 256u) return fail(c, DGN_ERR_INTERNAL, "partial EXEC mask at a Betti dequeue (DGN_EXEC_CHECK build)");
+    return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
+}
+
+// every deferred device-side report of this context (after a stream synchronization)
+int take_flags(dgn_ctx* c) {
+    if (int st = take_emit_flag(c)) {
+        (void)take_betti_flag(c);
+        return st;
+    }
+    return take_betti_flag(c);
+}
+
 GraphLaunch graph_launch(GraphWork& W, const dgn_batch* b, double rc, double eps, uint64_t kmax, bool use_mask) {
     return GraphLaunch{W.meta.as<StructMeta>(),  W.atom_struct.as<int32_t>(),
                        b->atom_offset,           b->positions,
@@ -299,7 +335,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->s, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    int st = take_emit_flag(c);
+    int st = take_flags(c);
     if (st) return st;
     if (c->host->s.graph_flag & kGErrFar)
         return fail(c, DGN_ERR_UNSUPPORTED, "an atom lies more than 500 lattice periods from the origin");
@@ -357,12 +393,12 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
 
 int check_emit_flag(dgn_ctx* c) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return take_emit_flag(c);
+    return take_flags(c);
 }
 
 int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int32_t* counts, const double* clouds,
                const int32_t* npoints, int32_t cloud_stride, int64_t num_clouds, float* pairs_out, int32_t pair_cap,
-               const float* lower = nullptr, bool reuse_graph = false) {
+               const float* lower = nullptr, bool reuse_graph = false, bool async_report = false) {
     const bool given = clouds || lower;
     const int64_t A = given ? num_clouds : b->num_atoms;
     auto nw = [&]() -> GraphWork& { return reuse_graph ? c->gw : c->bw; };
@@ -409,6 +445,11 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     HIP_TRY(c, c->scalars.ensure(sizeof(Scalars)));
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, 5 * sizeof(uint32_t), c->stream));
+    if (!c->bflags.p) {
+        HIP_TRY(c, c->bflags.ensure(kBFWords * sizeof(uint32_t)));
+        HIP_TRY(c, hipMemsetAsync(c->bflags.p, 0, kBFWords * sizeof(uint32_t), c->stream));
+    }
+    uint32_t* bflags = c->bflags.as<uint32_t>();
     HIP_TRY(c, c->b_list.ensure(sizeof(int32_t) * (size_t)A));
     // complexes above 64 points: the wide kernel, one wave per complex with a per-wave scratch
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
@@ -447,7 +488,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.thr = (float)rc;  // ripser_wrapper.cpp:28
     bl.features = features;
     bl.counts = counts;
-    bl.error_flag = &sc->error_flag;
+    bl.error_flag = bflags + kBFReduce;
     bl.work_counter = &sc->work_counter;
     bl.work_counter2 = &sc->work_counter2;
     bl.overflow_list = c->b_list.as<int32_t>();
@@ -542,16 +583,54 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         }
         // complexes whose reduction outgrew a kernel's workspace (the reference's Ripser has no
         // caps, ripser.cpp:514-1269): reduced again with the big wide layout
+        const int nmax = std::max(max_points, 64);
+        const bool coded = nmax > kWideRegular;
+        {
+            // Device-driven retry when a few big-layout waves fit a small budget (complexes of up to
+            // a few hundred points; the 5 A path): the launch reads the retry list's length on the
+            // device and its waves leave at once when nothing overflowed, so the pass never waits
+            // for the host. The workspace is kept (its tables restored by every reduction).
+            WideLayout big = betti_wide_layout(nmax, true);
+            const int64_t fit = (int64_t(4) << 30) / big.total;
+            const int64_t waves = std::min<int64_t>({fit, betti_wide_resident_waves(c->device, nmax), 64});
+            if (!coded && waves >= 8) {
+                if (c->big_nmax != nmax || c->big_waves < waves) {
+                    HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
+                    big.base = c->b_big.as<uint8_t>();
+                    HIP_TRY(c, betti_wide_init_scratch(c->stream, big, (int)waves));
+                    c->big_nmax = nmax;
+                    c->big_waves = (int)waves;
+                }
+                big.base = c->b_big.as<uint8_t>();
+                BettiLaunch rb = pb;
+                rb.rank_codes = nullptr;
+                rb.rank_sorted = nullptr;
+                rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
+                rb.retry_len = nullptr;
+                rb.force_retry = 0;
+                rb.retried = bflags + kBFRetried;
+                rb.wide_list = c->b_rlist.as<int32_t>();
+                rb.wide_len = &sc->retry_len;
+                rb.wide_queue = &sc->retry_queue;
+                {
+                    TimedLaunch t(c, "betti_retry", 0.0, 0.0);
+                    HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)waves));
+                }
+                HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
+                return DGN_OK;
+            }
+        }
+        // larger complexes: the retry workspace is sized by the number of complexes that overflowed
+        // (one host read of the list length)
         HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         const int64_t nretry = c->host->s.retry_len;
         if (nretry == 0) return DGN_OK;
-        // complexes above kWideRegular points (listed by the regular wide launch) run on rank codes
+        // complexes above kWideRegular points (listed by the bucket pass) run on rank codes
         // (betti_rank_codes, the BIG instantiation), in slices of at most 512 complexes
-        const int nmax = std::max(max_points, 64);
-        const bool coded = nmax > kWideRegular;
         WideLayout big = betti_wide_layout(nmax, true);
+        c->big_nmax = 0;  // the workspace below is laid out per call
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t rstride = ((int64_t)nmax * (nmax - 1) / 2 + 63) / 64 * 64;
@@ -576,6 +655,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
         rb.retry_len = nullptr;
         rb.force_retry = 0;
+        rb.retried = bflags + kBFRetried;
         std::vector<uint32_t> lens;
         for (int64_t r0 = 0; r0 < nretry; r0 += slice) {
             const int64_t cnt = std::min<int64_t>(slice, nretry - r0);
@@ -641,7 +721,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 } else {
                     HIP_TRY(c, launch_betti_dist_search(c->stream, g, c0, cnt, max_points, tri_stride,
                                                         nw().counts.as<int32_t>(), c->b_lower.as<float>(),
-                                                        c->b_np.as<int32_t>(), &sc->graph_flag));
+                                                        c->b_np.as<int32_t>(), bflags + kBFSearch));
                 }
             }
             // Betti pass: triangles in, 35 f64 + 4 i32 out
@@ -651,22 +731,19 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             if (st) return st;
         }
     }
-    HIP_TRY(c, hipMemcpyAsync(&c->host->s.graph_flag, &sc->graph_flag, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              c->stream));
+    // the pass's flags travel to the host behind its work; the device entry points return here
+    // (asynchronous: the next synchronizing call reports them), the host ones wait and report
+    HIP_TRY(c, hipMemcpyAsync(c->host->betti_flags, bflags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    c->betti_pending = true;
+#ifdef DGN_PHASE_TIMING
+    async_report = false;
+#endif
+    if (async_report) return DGN_OK;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, hipMemcpy(c->phase_host, c->phase.p, sizeof(c->phase_host), hipMemcpyDeviceToHost));
 #endif
-    if (int st = take_emit_flag(c)) return st;
-    if (c->host->s.graph_flag)
-        return fail(c, DGN_ERR_INTERNAL,
-                    "Betti neighbour search disagreed with the count pass (flags " + std::to_string(c->host->s.graph_flag) + ")");
-    const uint32_t f = c->host->s.error_flag;
-    if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
-    if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
-    if (f & 256u) return fail(c, DGN_ERR_INTERNAL, "partial EXEC mask at a Betti dequeue (DGN_EXEC_CHECK build)");
-    if (f) return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
-    return DGN_OK;
+    return take_flags(c);
 }
 
 // stage a host batch into context-owned device buffers
@@ -761,7 +838,7 @@ int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
     // a graph emit's consistency flag is still being copied on the old stream: let it land before
     // the stream is swapped, so the next synchronizing call reads it (take_emit_flag syncs only
     // the current stream)
-    if (c->emit_pending) HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->emit_pending || c->betti_pending) HIP_TRY(c, hipStreamSynchronize(c->stream));
     // NULL (the legacy null stream, e.g. torch's default stream) -> the context's own blocking
     // stream, which the null stream orders against; anything else is used as given
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
@@ -782,7 +859,21 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
 int dgn_ctx_synchronize(dgn_ctx* c) {
     if (!c) return DGN_ERR_ARG;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return take_emit_flag(c);  // a pending graph-emit consistency failure surfaces here
+    return take_flags(c);  // a pending graph-emit or Betti failure surfaces here
+}
+
+int dgn_debug_retry_count(dgn_ctx* c, int64_t* out) {
+    if (!c || !out) return DGN_ERR_ARG;
+    *out = 0;
+    if (!c->bflags.p) return DGN_OK;
+    uint32_t v = 0;
+    HIP_TRY(c, hipMemcpyAsync(&c->host->pad, c->bflags.as<uint32_t>() + kBFRetried, sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->bflags.as<uint32_t>() + kBFRetried, 0, sizeof(uint32_t), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    v = c->host->pad;
+    *out = v;
+    return take_flags(c);
 }
 
 const char* dgn_ctx_last_error(const dgn_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
@@ -928,7 +1019,7 @@ int dgn_dev_betti(dgn_ctx* c, const dgn_batch* b, const dgn_betti_params* p, dou
     if (!c || !p || !batch_ok(b) || !b->species || !features || !(p->r_cutoff > 0))
         return fail(c, DGN_ERR_ARG, "dgn_dev_betti: bad args");
     HIP_TRY(c, hipSetDevice(c->device));
-    return betti_impl(c, b, p->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0);
+    return betti_impl(c, b, p->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0, nullptr, false, true);
 }
 
 int dgn_dev_graph_betti(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* p, int64_t* row_ptr,
@@ -944,7 +1035,7 @@ int dgn_dev_graph_betti(dgn_ctx* c, const dgn_batch* b, const dgn_graph_params* 
     // (the 1/count(species) weights are reused only for the species array the count saw)
     const bool reuse = bp->r_cutoff == p->r_cutoff && p->epsilon == 1e-10 && c->gw.has_weight &&
                        c->gw.species == b->species;
-    return betti_impl(c, b, bp->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0, nullptr, reuse);
+    return betti_impl(c, b, bp->r_cutoff, features, counts, nullptr, nullptr, 0, 0, nullptr, 0, nullptr, reuse, true);
 }
 
 int dgn_dev_node_features(dgn_ctx* c, const dgn_batch* b, const double* embed, int32_t num_keys, int32_t D,

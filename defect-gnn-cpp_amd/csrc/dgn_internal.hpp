@@ -113,7 +113,8 @@ struct BettiLaunch {
     // (null = report DGN_ERR_CAPACITY) and reduced again by betti_wide_kernel with the big layout
     int32_t* retry_list;      // [num_atoms]
     uint32_t* retry_len;
-    int32_t force_retry;      // tests (DGN_FORCE_RETRY=1): the host lists every complex for the retry launch
+    int32_t force_retry;      // tests (DGN_DEBUG_FORCE_RETRY): the host lists every complex for the retry launch
+    uint32_t* retried;        // capacity-retry launches: +1 per complex reduced (diagnostics counter), or null
     // complexes above kWideRegular points (the retry launch's BIG wide instantiation): per retry
     // slot r, rank codes of the packed lower triangle and the sorted f32 distances (betti_rank_codes)
     const uint32_t* rank_codes;  // [slots][rank_stride]

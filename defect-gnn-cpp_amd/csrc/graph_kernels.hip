@@ -1124,11 +1124,17 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
         T* ob = o - phase;
         for (int v = v0 + lane; v < nfull; v += kWave) {
             const vec_t val = *reinterpret_cast<const DGN_LDS vec_t*>(buf + V * v);
+            // f32: non-temporal 16-byte stores; f64 (the reference's edge_attr dtype, twice the
+            // bytes): plain stores, which the L2 merges into full lines -- measured on the fused
+            // emit, config-4 shard: f64 4.01 -> 3.46 ms with plain stores, f32 2.23 -> 2.37 ms
+            // (worse) with them (tools/r03_graph_exp.sh)
 #ifdef DGN_RBF_PLAIN_STORE
-            *reinterpret_cast<vec_t*>(ob + V * v) = val;
+            constexpr bool plain = true;
 #else
-            __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(ob + V * v));
+            constexpr bool plain = sizeof(T) == 8;
 #endif
+            if constexpr (plain) *reinterpret_cast<vec_t*>(ob + V * v) = val;
+            else __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(ob + V * v));
         }
         if (lane < V) {
             const int fh = lane, ft = V * nfull + lane;  // head unit 0 (phase > 0), tail unit nfull

@@ -23,7 +23,7 @@ EXPORTS = [
     "dgn_graph_result_free", "dgn_dev_betti", "dgn_host_betti", "dgn_host_persistence",
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
-    "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug",
+    "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug", "dgn_debug_retry_count",
 ]
 DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP = 1, 2, 3, 4
 
@@ -99,6 +99,8 @@ def lib():
     L.dgn_ctx_synchronize.argtypes = [vp]
     if hasattr(L, "dgn_ctx_set_debug"):  # absent from older A/B builds
         L.dgn_ctx_set_debug.argtypes = [vp, C.c_int, C.c_int]
+    if hasattr(L, "dgn_debug_retry_count"):
+        L.dgn_debug_retry_count.argtypes = [vp, C.POINTER(i64)]
     L.dgn_ctx_last_error.restype = C.c_char_p
     L.dgn_ctx_last_error.argtypes = [vp]
     L.dgn_ctx_enable_timing.argtypes = [vp, C.c_int]
@@ -212,6 +214,12 @@ class Context:
     def set_debug(self, knob: int, value: int):
         """Debug / A-B knob (DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16); tests and tools only."""
         self._check(lib().dgn_ctx_set_debug(self.h, knob, value), "set_debug")
+
+    def retry_count(self) -> int:
+        """Complexes the capacity-retry launches reduced since the last call (synchronizes)."""
+        n = C.c_int64()
+        self._check(lib().dgn_debug_retry_count(self.h, C.byref(n)), "retry_count")
+        return n.value
 
     def synchronize(self):
         self._check(lib().dgn_ctx_synchronize(self.h), "synchronize")

@@ -58,6 +58,8 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps. */
 enum { DGN_DEBUG_FORCE_RETRY = 1, DGN_DEBUG_WIDE_WAVES = 2, DGN_DEBUG_WIDE_C16 = 3, DGN_DEBUG_WIDE_CAP = 4 };
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
+/* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */
+int dgn_debug_retry_count(dgn_ctx* ctx, int64_t* count);
 const char* dgn_ctx_last_error(const dgn_ctx* ctx);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream around every launch. */
@@ -151,12 +153,19 @@ typedef struct {
     double r_cutoff; /* reference default 10.0 */
 } dgn_betti_params;
 
+/* dgn_dev_betti synchronizes once, after its own neighbour count (the local complexes' size sets the
+ * kernel tier and workspaces); the Betti kernels then run asynchronously and their error status
+ * (envelope, workspace overflow of a retried complex, a search/count disagreement) is returned by the
+ * next synchronizing call on the context (dgn_ctx_synchronize, dgn_dev_graph_count, a dgn_host_*
+ * call); the affected atoms' features are NaN and their counts -1 either way. */
 int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* p, double* features,
                   int32_t* counts);
 int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
                    double* features, int32_t* counts);
 
-/* Fused step (device, async except for the Betti pass's final flag read): dgn_dev_graph_emit of a
+/* Fused step (device, asynchronous: no host synchronization for complexes of up to a few hundred
+ * points -- larger ones size their capacity-retry workspace from one host read; errors are reported
+ * by the next synchronizing call as for dgn_dev_betti): dgn_dev_graph_emit of a
  * preceding dgn_dev_graph_count, then dgn_dev_betti on the same batch. When the Betti cutoff equals
  * the graph cutoff (and epsilon is the default 1e-10) the Betti pass reuses the graph count's
  * per-atom neighbour counts and hit masks instead of searching a third time: CrystalGraph's

@@ -18,11 +18,11 @@ def _ref(low, n, thr):
 
 
 def _check(ctx, clouds, npts, thr, cap):
-    ctx.reset_timing()
-    ctx.enable_timing(True)
+    """Pairs and counts vs verbatim Ripser; returns the number of complexes the capacity-retry launch
+    reduced (dgn_debug_retry_count: the retry launch itself runs on every pass, device-driven)."""
+    ctx.retry_count()
     pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=cap)
-    kt = ctx.kernel_times()
-    ctx.enable_timing(False)
+    kt = ctx.retry_count()
     bad = []
     for c in range(len(npts)):
         n = int(npts[c])
@@ -39,12 +39,10 @@ def _check(ctx, clouds, npts, thr, cap):
 
 def _check_lower(ctx, lowers, npts, thr, cap):
     """host_persistence_lower (compute_persistence_from_distances) on caller-given f32 triangles."""
-    ctx.reset_timing()
-    ctx.enable_timing(True)
+    ctx.retry_count()
     maxp = int(max(npts))
     pairs, counts = ctx.host_persistence_lower(lowers, npts, maxp, thr, cap=cap)
-    kt = ctx.kernel_times()
-    ctx.enable_timing(False)
+    kt = ctx.retry_count()
     bad = []
     for c in range(len(npts)):
         n = int(npts[c])
@@ -85,7 +83,7 @@ def test_clique_200_points(ctx):
     rng = np.random.default_rng(37)
     clouds, npts = _cliques(rng, [200])
     kt = _check(ctx, clouds, npts, 2.0, 1 << 17)
-    assert "betti_retry" not in kt, kt
+    assert kt == 0, kt
 
 
 def test_forced_capacity_retry_all_tiers(ctx):
@@ -101,9 +99,9 @@ def test_forced_capacity_retry_all_tiers(ctx):
         kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
     finally:
         ctx.set_debug(dgn.abi.DEBUG_FORCE_RETRY, 0)
-    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    assert kt >= 1, kt
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.9, 4096)
-    assert "betti_retry" not in kt
+    assert kt == 0, kt
 
 
 @pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
@@ -118,7 +116,7 @@ def test_cloud_above_512_points(ctx):
         clouds[c, :n] = rng.uniform(0, 9.0 * (n / 700) ** (1 / 3), size=(n, 3))
     clouds[2, 10] = clouds[2, 3]  # a duplicate point: zero distance, dim-0 pair not emitted
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.6, 1 << 14)
-    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    assert kt >= 1, kt
 
 
 @pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
@@ -151,7 +149,7 @@ def test_natural_retry_narrow_clouds(ctx):
     clouds[2, :48] = np.stack([np.cos(t), np.sin(t), 0.01 * rng.standard_normal(48)], 1)
     clouds[3, :30] = rng.uniform(0, 1.0, size=(30, 3))  # an ordinary complex in the same batch
     kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 3.0, 1 << 12)
-    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    assert kt >= 1, kt
 
 
 def test_natural_retry_narrow_matrices(ctx):
@@ -166,7 +164,7 @@ def test_natural_retry_narrow_matrices(ctx):
         M = rng.uniform(0.0, 1.0, (n, n)) if kind == "uniform" else rng.integers(1, 5, (n, n)).astype(np.float64)
         lowers[c, :n * (n - 1) // 2] = np.array([M[i, j] for i in range(1, n) for j in range(i)], np.float32)
     kt = _check_lower(ctx, lowers, np.array(sizes, dtype=np.int32), 5.0, 1 << 12)
-    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    assert kt >= 1, kt
 
 
 def test_wide_in_kernel_overflow_retry(ctx):
@@ -188,6 +186,6 @@ def test_wide_in_kernel_overflow_retry(ctx):
         kt = _check(ctx, clouds, npts, 2.0, 4096)
     finally:
         ctx.set_debug(dgn.abi.DEBUG_WIDE_CAP, 0)
-    assert kt.get("betti_retry", {}).get("launches", 0) >= 1, kt
+    assert kt >= 1, kt
     kt = _check(ctx, clouds, npts, 2.0, 4096)  # natural caps again: no retry
-    assert "betti_retry" not in kt, kt
+    assert kt == 0, kt

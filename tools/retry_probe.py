@@ -19,8 +19,7 @@ def tri_from_matrix(M):
 
 
 def run(ctx, name, lowers, npts, thr, maxp):
-    ctx.reset_timing()
-    ctx.enable_timing(True)
+    ctx.retry_count()
     t0 = time.perf_counter()
     try:
         pairs, counts = ctx.host_persistence_lower(lowers, npts, maxp, thr, cap=1 << 16)
@@ -28,9 +27,7 @@ def run(ctx, name, lowers, npts, thr, maxp):
     except Exception as e:  # noqa: BLE001
         counts, st = None, str(e)[:120]
     dt = time.perf_counter() - t0
-    kt = ctx.kernel_times()
-    ctx.enable_timing(False)
-    print(f"{name:34s} retry={kt.get('betti_retry', {}).get('launches', 0)} {dt:7.3f}s {st} "
+    print(f"{name:34s} retried={ctx.retry_count()} {dt:7.3f}s {st} "
           f"counts={None if counts is None else counts.tolist()[:3]}", flush=True)
 
 
