@@ -716,6 +716,11 @@ struct Complex {
 template <int NP>
 __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
+#ifdef DGN_OCC_PAD
+    // A/B diagnostics only: extra LDS per wave to lower the occupancy (occupancy sensitivity)
+    __shared__ uint32_t occ_pad[DGN_OCC_PAD];
+    if (lane_id() == 0) occ_pad[blockIdx.x % DGN_OCC_PAD] = 0u;
+#endif
 #ifdef DGN_PHASE_TIMING
     // diagnostics counters in LDS (registers would change the kernel's occupancy)
     __shared__ uint64_t ph[32];

@@ -256,8 +256,9 @@ struct WideCx {
                                     uint64_t& bestp, int& bk, bool& found, uint32_t& hda, uint32_t& hdb,
                                     uint32_t& hdc, int* steps = nullptr) const {
         uint64_t best = kInfW;
+        uint32_t bd = 0xFFFFFFFFu;
         found = false;
-        bk = 0;
+        bk = -1;
         bestp = 0;
         // candidates popped highest first, four per step so their distance reads are in flight
         // together (scratch reads: the latency, not the bandwidth, is what a lane waits for)
@@ -289,32 +290,31 @@ struct WideCx {
                 dbv[j] = d(b, k);
                 dc[j] = dim == 2 ? d(c, k) : 0u;
             }
+            // walking k downwards, a later (smaller) k wins only with a strictly smaller diameter
+            // (inserting a larger vertex gives the larger combinatorial index, i.e. the F-smaller
+            // key at equal diameter): only (diameter, k) are tracked, the winner's key is built once
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (!val[j] || found) continue;
                 const int k = kk[j];
                 const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
-                const uint64_t p = pinsert(dim + 1, sp_, k);
-                const uint64_t idx = pidx(dim + 2, p);
                 if (dk <= dsig) {
-                    best = wkey(dsig, idx);
-                    bestp = p;
+                    bd = dsig;
                     bk = k;
                     found = true;
                     hda = da[j];
                     hdb = dbv[j];
                     hdc = dc[j];
-                } else {
-                    const uint64_t kk2 = wkey(dk, idx);
-                    if (kk2 < best) {
-                        best = kk2;
-                        bestp = p;
-                        bk = k;
-                    }
+                } else if (dk < bd) {
+                    bd = dk;
+                    bk = k;
                 }
             }
             if (found || !val[3]) break;
         }
+        if (bk < 0) return kInfW;
+        bestp = pinsert(dim + 1, sp_, bk);
+        best = wkey(bd, pidx(dim + 2, bestp));
         return best;
     }
 
@@ -395,7 +395,8 @@ struct WideCx {
         uint64_t tm = 0;              // remaining c of that word
         bool act = false, fresh = false;
         int c = 0, w = 0, bk = 0;
-        uint64_t m = 0, tidx = 0, best = kInfW, bestp = 0;
+        uint64_t m = 0, tidx = 0;
+        uint32_t bd = 0xFFFFFFFFu;  // diameter of the best cofacet of the lane's triangle so far
         uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, colp = 0, hda = 0, hdb = 0, hdc = 0;
         bool found = false;
 #ifdef DGN_PHASE_TIMING
@@ -436,9 +437,8 @@ struct WideCx {
                 colp = ((uint32_t)ea << (2 * VB)) | ((uint32_t)eb << VB) | (uint32_t)c;
                 w = W - 1;
                 m = aw(ea, w) & aw(eb, w) & aw(c, w);
-                best = kInfW;
-                bestp = 0;
-                bk = 0;
+                bd = 0xFFFFFFFFu;
+                bk = -1;
                 found = false;
             }
             if (!ballot(act)) break;
@@ -486,35 +486,33 @@ struct WideCx {
                     mc_t[tidx] = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
                     done = true;
                 } else {
+                    // (diameter, k) only, as in min_cofacet: a smaller k wins only with a strictly
+                    // smaller diameter; the winner's key is built when the walk ends
 #pragma unroll
                     for (int j = 0; j < kStep; ++j) {
                         if (!val[j] || found) continue;
                         const int k = kk[j];
                         const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
-                        const uint64_t p = pinsert(3, colp, k);
-                        const uint64_t idx = pidx(4, p);
                         if (dk <= ds) {
-                            best = wkey(ds, idx);
-                            bestp = p;
+                            bd = ds;
                             bk = k;
                             found = true;
                             hda = da[j];
                             hdb = dbv[j];
                             hdc = dc[j];
-                        } else {
-                            const uint64_t kk2 = wkey(dk, idx);
-                            if (kk2 < best) {
-                                best = kk2;
-                                bestp = p;
-                                bk = k;
-                            }
+                        } else if (dk < bd) {
+                            bd = dk;
+                            bk = k;
                         }
                     }
                     done = found || !val[kStep - 1];
                     if (done) {
                         // apparent iff (a, b, c) is the F-max facet of its zero-persistence cofacet
                         uint16_t mc = kMcNoneW;
-                        if (best != kInfW) {
+                        uint64_t best = kInfW, bestp = 0;
+                        if (bk >= 0) {
+                            bestp = pinsert(3, colp, bk);
+                            best = wkey(bd, pidx(4, bestp));
                             const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
                                              (bk > b || max(max(hda, hdc), dac) < ds) &&
                                              (bk > c || max(max(hda, hdb), dab) < ds);

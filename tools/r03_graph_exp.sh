@@ -5,7 +5,7 @@ set -eo pipefail
 OUT=gpurun_out/${EXP_TAG:-r03_graph_exp}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for dt in f64 f32; do
+for dt in ${DTYPES:-f64 f32}; do
   for v in ${VARIANTS:-libdgn libdgn_split libdgn_norbf}; do
     DGN_LIB=defect-gnn-cpp_amd/lib/$v.so timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tr_${v}_$dt" -o run -- \
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-betti --no-alt-rbf --rbf-dtype $dt > "$OUT/b_${v}_$dt.log" 2>&1
