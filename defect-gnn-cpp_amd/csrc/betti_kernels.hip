@@ -87,17 +87,24 @@ struct ScratchLayout {
     static constexpr int64_t mincof_e = mincof + (64 * 63 * 62 / 6);  // uint8 [C(64,2)] edges
     static constexpr int64_t edges = (mincof_e + (64 * 63 / 2) + 15) / 16 * 16;  // uint16 [C(64,2)] (i << 8 | j)
     static constexpr int64_t tris = (edges + 2 * (64 * 63 / 2) + 15) / 16 * 16;  // uint32 [C(64,3)] packed triangles
-    static constexpr int64_t total = tris + 4 * (64 * 63 * 62 / 6);
+    static constexpr int64_t d0 = tris + 4 * (64 * 63 * 62 / 6);    // f32 [64] dim-0 deaths
+    static constexpr int64_t total = d0 + 4 * 64;
 };
 
+// Per-wave LDS. The tiers are sized for resident waves: NP = 44 (the typical 5 A complex of
+// 43..44 points) fits 8 KB, i.e. 20 waves per CU (5 per SIMD, with __launch_bounds__ capping the
+// VGPRs at 96), where NP = 48 (9.6 KB) keeps 16. The hot reads (rows a, b, c at column k =
+// lane) are conflict-free for any stride; an odd stride also makes column reads conflict-free,
+// kept where it costs no occupancy step.
 template <int NP>
 struct BettiSmem {
-    static constexpr int S = NP + 1;  // odd row stride: row and column reads are conflict-free
+    static constexpr int S = NP == 44 ? NP : NP + 1;
     float D[NP * S];                  // full symmetric f32 distance matrix, D[i * S + j]
     uint64_t adj[NP];
-    float d0[NP];
     uint8_t par[NP];                  // minimum spanning forest: parent of each vertex (0xFF = root)
 };
+template <int NP>
+constexpr int betti_waves_per_simd() { return NP <= 44 ? 5 : (NP <= 48 ? 4 : 3); }
 
 // ---------------------------------------------------------------------------------------
 // small helpers
@@ -223,9 +230,9 @@ struct Complex {
     __device__ uint32_t db(int i, int j) const { return Db()[i * S + j]; }
     __device__ float dlow(int a, int b) const { return __uint_as_float(dlowb(a, b)); }
     __device__ float dist(int i, int j) const { return __uint_as_float(db(i, j)); }
-    __device__ uint64_t ekey(int i, int j) const {  // i != j
+    __device__ uint64_t ekey(int i, int j) const {  // i != j; reads row i (Prim: i uniform)
         const int a = max(i, j), b = min(i, j);
-        return make_key(dlow(a, b), pack2(a, b));
+        return make_key(dist(i, j), pack2(a, b));
     }
     __device__ uint32_t tri_diamb(int a, int b, int c) const {  // a > b > c
         return max(max(dlowb(a, b), dlowb(a, c)), dlowb(b, c));
@@ -714,7 +721,7 @@ struct Complex {
 #endif
 
 template <int NP>
-__global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLaunch bl) {
+__global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
 #ifdef DGN_OCC_PAD
     // A/B diagnostics only: extra LDS per wave to lower the occupancy (occupancy sensitivity)
@@ -734,7 +741,7 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
     const int64_t A = bl.num_atoms;
 
     // complexes of this launch: all of them, or the overflow list written by the bucket pass
-    const int64_t total = bl.work_list ? (int64_t)*bl.overflow_len : A;
+    const int64_t total = bl.work_list ? (int64_t)*bl.work_len : A;
     for (;;) {
 #ifdef DGN_EXEC_CHECK
         // diagnostics: every lane must be live at the dequeue
@@ -823,6 +830,7 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
                 if (lane < NP) s.par[lane] = 0xFF;
             }
             lds_sync();
+            float* d0s = cx.template sp<float>(ScratchLayout::d0);
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
             cx.n_d0 = 0;
@@ -848,7 +856,7 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
                         const int u = __shfl(parent, v, kWave);
                         const float dd = key_diam(kmin);
                         if (dd != 0.0f) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
-                            if (lane == 0) s.d0[cx.n_d0] = dd;
+                            if (lane == 0) d0s[cx.n_d0] = dd;
                             cx.n_d0 += 1;
                         }
                         if (lane == 0) s.par[v] = (uint8_t)u;
@@ -1088,11 +1096,11 @@ __global__ __launch_bounds__(kWave, NP <= 48 ? 4 : 3) void betti_kernel(BettiLau
                 if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
             } else {
                 // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
-                const double myval = betti_stats35(s.d0, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
+                const double myval = betti_stats35(d0s, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
                 if (feat && lane < 35) feat[lane] = myval;
                 if (bl.pairs_out) {
                     float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;
-                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, s.d0[i]);
+                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, d0s[i]);
                     for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) po[bl.pair_cap + i] = cx.pairs(1)[i];
                     for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) po[2 * bl.pair_cap + i] = cx.pairs(2)[i];
                 }
@@ -1166,7 +1174,9 @@ hipError_t betti_init_scratch(hipStream_t s, uint8_t* base, int slots) {
     return hipMemset2DAsync(base + ScratchLayout::mincof, (size_t)ScratchLayout::total, kMcNone, width, (size_t)slots, s);
 }
 
-static int np_for(int max_points) { return max_points <= 32 ? 32 : (max_points <= 48 ? 48 : 64); }
+static int np_for(int max_points) {
+    return max_points <= 32 ? 32 : (max_points <= 44 ? 44 : (max_points <= 48 ? 48 : 64));
+}
 
 int betti_grid_waves(int device) {
     hipDeviceProp_t prop;
@@ -1178,12 +1188,23 @@ int betti_grid_waves(int device) {
     return prop.multiProcessorCount * per_cu;
 }
 
-// route complexes above np_small points: up to 64 to the overflow list (NP = 64 launch), above
-// 64 to the wide list (betti_wide_kernel); wave-aggregated appends
-__global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small) {
+// route complexes above np_small points: up to np_mid to the mid list (NP = 48 launch), up to
+// 64 to the overflow list (NP = 64 launch), above 64 to the wide list (betti_wide_kernel);
+// wave-aggregated appends
+__device__ __forceinline__ void bucket_append(bool take, int32_t* list, uint32_t* len, int64_t gi) {
+    const uint64_t b = ballot(take);
+    if (!b) return;
+    const int leader = __ffsll((unsigned long long)b) - 1;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(len, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, leader, kWave);
+    if (take) list[base + mask_prefix(b)] = (int32_t)gi;
+}
+__global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small, int np_mid) {
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int n = gi < bl.num_atoms ? bl.npoints[gi] : 0;
-    const bool mid = gi < bl.num_atoms && n > np_small && n <= 64;
+    const bool tier48 = gi < bl.num_atoms && n > np_small && n <= np_mid;
+    const bool mid = gi < bl.num_atoms && n > np_mid && n <= 64;
     // above kWideRegular points: straight to the retry list (rank-coded BIG launch)
 #ifdef DGN_HANG_REPRO
     const bool huge = false;  // diagnostics: the regular wide launch meets them (its skip path)
@@ -1191,28 +1212,10 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     const bool huge = gi < bl.num_atoms && n > kWideRegular && bl.retry_list;
 #endif
     const bool wide = gi < bl.num_atoms && n > 64 && !huge;
-    const uint64_t bm = ballot(mid), bw = ballot(wide), bh = ballot(huge);
-    if (bh) {
-        const int leader = __ffsll((unsigned long long)bh) - 1;
-        uint32_t base = 0;
-        if (lane_id() == leader) base = atomicAdd(bl.retry_len, (uint32_t)__popcll(bh));
-        base = (uint32_t)__shfl((int)base, leader, kWave);
-        if (huge) bl.retry_list[base + mask_prefix(bh)] = (int32_t)gi;
-    }
-    if (bm) {
-        const int leader = __ffsll((unsigned long long)bm) - 1;
-        uint32_t base = 0;
-        if (lane_id() == leader) base = atomicAdd(bl.overflow_len, (uint32_t)__popcll(bm));
-        base = (uint32_t)__shfl((int)base, leader, kWave);
-        if (mid) bl.overflow_list[base + mask_prefix(bm)] = (int32_t)gi;
-    }
-    if (bw) {
-        const int leader = __ffsll((unsigned long long)bw) - 1;
-        uint32_t base = 0;
-        if (lane_id() == leader) base = atomicAdd(bl.wide_len, (uint32_t)__popcll(bw));
-        base = (uint32_t)__shfl((int)base, leader, kWave);
-        if (wide) bl.wide_list[base + mask_prefix(bw)] = (int32_t)gi;
-    }
+    bucket_append(huge, bl.retry_list, bl.retry_len, gi);
+    bucket_append(tier48, bl.mid_list, bl.mid_len, gi);
+    bucket_append(mid, bl.overflow_list, bl.overflow_len, gi);
+    bucket_append(wide, bl.wide_list, bl.wide_len, gi);
 }
 
 // device facts for the persistent grids, queried once per device (hipGetDeviceProperties is a
@@ -1252,6 +1255,7 @@ static int grid_np(int grid_waves, int64_t max_items) {
 
 static int grid_for(int np, int grid_waves, int64_t max_items) {
     if (np == 32) return grid_np<32>(grid_waves, max_items);
+    if (np == 44) return grid_np<44>(grid_waves, max_items);
     if (np == 48) return grid_np<48>(grid_waves, max_items);
     return grid_np<64>(grid_waves, max_items);
 }
@@ -1264,34 +1268,37 @@ static hipError_t launch_np(hipStream_t st, const BettiLaunch& b, int grid) {
 
 static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int grid) {
     if (np == 32) return launch_np<32>(st, b, grid);
+    if (np == 44) return launch_np<44>(st, b, grid);
     if (np == 48) return launch_np<48>(st, b, grid);
     return launch_np<64>(st, b, grid);
 }
 
-// Three-level dispatch: the main launch uses the instantiation sized for typical complexes
-// (NP <= 48: about half the LDS of NP = 64, so twice the resident waves); complexes above it
-// are listed by betti_bucket_kernel and reduced by an NP = 64 launch (49..64 points) and by
-// betti_wide_kernel (65..512 points). Counters and list lengths live on the device, so nothing
-// synchronizes with the host in between.
+// Tiered dispatch: the main launch uses the instantiation sized for typical complexes (NP = 44:
+// 20 resident waves per CU); complexes above it are listed by betti_bucket_kernel and reduced by
+// an NP = 48 launch (45..48 points, 16 waves per CU) after the main one, an NP = 64 launch
+// (49..64 points) forked beside it, and betti_wide_kernel (65..512 points). Counters and list
+// lengths live on the device, so nothing synchronizes with the host in between.
 hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
                         int wide_waves, const BettiFork* fork) {
     const int np_big = np_for(max_points < 64 ? max_points : 64);
-    const int np_main = np_big > 48 ? 48 : np_big;
+    const int np_main = np_big > 44 ? 44 : np_big;
+    const int np_mid = np_big > 44 ? 48 : np_main;  // tier 48 only when the main tier is 44
     BettiLaunch m = b;
     m.work_list = nullptr;
     m.queue = b.work_counter;
     m.skip_above = max_points > np_main ? 1 : 0;
     if (m.skip_above) {
         const int64_t blocks = (b.num_atoms + 255) / 256;
-        hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main);
+        hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main, np_mid);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    // scratch slots [0, main_grid) belong to the main launch
+    // scratch slots [0, main_grid) belong to the main launch (and then to the mid launch)
     const int main_grid = grid_for(np_main, fork ? grid_waves - fork->overflow_waves : grid_waves, b.num_atoms);
-    const bool overflow = m.skip_above && np_big > np_main;
+    const bool overflow = m.skip_above && np_big > 48;
     BettiLaunch o = b;
     o.work_list = b.overflow_list;
+    o.work_len = b.overflow_len;
     o.queue = b.work_counter2;
     o.skip_above = 0;
     hipError_t e;
@@ -1300,19 +1307,27 @@ hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, in
         // launch they would add one heavy complex's latency to the pass. Instead they run on a
         // forked stream beside the main launch, on scratch slots past the main grid's.
         o.scratch = b.scratch + (int64_t)main_grid * b.scratch_per_wave;
-        const int og = grid_for(np_big, fork->overflow_waves, b.num_atoms);
+        const int og = grid_for(64, fork->overflow_waves, b.num_atoms);
         if ((e = hipEventRecord(fork->fork, st)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(fork->side, fork->fork, 0)) != hipSuccess) return e;
-        if ((e = launch_for(np_big, fork->side, o, og)) != hipSuccess) return e;
+        if ((e = launch_for(64, fork->side, o, og)) != hipSuccess) return e;
         if ((e = hipEventRecord(fork->join, fork->side)) != hipSuccess) return e;
     }
     e = launch_for(np_main, st, m, main_grid);
     if (e != hipSuccess || !m.skip_above) return e;
+    if (np_mid > np_main) {
+        BettiLaunch t = b;
+        t.work_list = b.mid_list;
+        t.work_len = b.mid_len;
+        t.queue = b.work_counter3;
+        t.skip_above = 0;
+        if ((e = launch_for(48, st, t, grid_for(48, main_grid, b.num_atoms))) != hipSuccess) return e;
+    }
     if (overflow) {
         if (fork) {
             if ((e = hipStreamWaitEvent(st, fork->join, 0)) != hipSuccess) return e;
         } else {
-            e = launch_for(np_big, st, o, grid_for(np_big, grid_waves, b.num_atoms));
+            e = launch_for(64, st, o, grid_for(64, grid_waves, b.num_atoms));
             if (e != hipSuccess) return e;
         }
     }

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,7 +76,8 @@ struct Scalars {  // device-side scalars, one allocation
     uint32_t wide_len;          // complexes routed to the wide launch
     uint32_t retry_len;         // complexes routed to the capacity-retry launch
     uint32_t retry_queue;       // capacity-retry launch queue
-    uint32_t pad[2];
+    uint32_t mid_len;           // complexes routed to the mid (NP = 48) launch
+    uint32_t work_counter3;     // betti mid launch queue
 };
 
 // one neighbour pass's device workspace and the facts its count recorded (count -> emit handshake)
@@ -450,7 +452,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         HIP_TRY(c, hipMemsetAsync(c->bflags.p, 0, kBFWords * sizeof(uint32_t), c->stream));
     }
     uint32_t* bflags = c->bflags.as<uint32_t>();
-    HIP_TRY(c, c->b_list.ensure(sizeof(int32_t) * (size_t)A));
+    HIP_TRY(c, c->b_list.ensure(2 * sizeof(int32_t) * (size_t)A));  // overflow list, mid list
     // complexes above 64 points: the wide kernel, one wave per complex with a per-wave scratch
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
     WideLayout wl{};
@@ -493,6 +495,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.work_counter2 = &sc->work_counter2;
     bl.overflow_list = c->b_list.as<int32_t>();
     bl.overflow_len = &sc->overflow_len;
+    bl.mid_list = c->b_list.as<int32_t>() + A;
+    bl.mid_len = &sc->mid_len;
+    bl.work_counter3 = &sc->work_counter3;
     bl.scratch = c->b_scratch.as<uint8_t>();
     bl.scratch_per_wave = spw;
     bl.clouds = clouds;
@@ -524,7 +529,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.features = features ? features + 35 * c0 : nullptr;
         pb.counts = counts ? counts + 4 * c0 : nullptr;
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
-        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 7 * sizeof(uint32_t), c->stream));
+        static_assert(offsetof(Scalars, work_counter3) - offsetof(Scalars, work_counter) == 8 * sizeof(uint32_t),
+                      "queue and list counters are contiguous");
+        HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 9 * sizeof(uint32_t), c->stream));
         // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
         // the scattered walk and pivot-search reads miss on): the narrow launches and the bucket
         // pass first, then per slice of the wide list its codes (betti_rank_codes) and a wide launch

@@ -86,6 +86,10 @@ struct BettiLaunch {
     // on the low-occupancy instantiation)
     int32_t* overflow_list;   // [num_atoms]
     uint32_t* overflow_len;
+    // 45..48-point complexes (NP = 48 launch after the NP = 44 main launch)
+    int32_t* mid_list;        // [num_atoms]
+    uint32_t* mid_len;
+    uint32_t* work_counter3;  // persistent work queue (mid launch)
     uint8_t* scratch;         // per-wave global scratch
     int64_t scratch_per_wave;
     // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
@@ -107,6 +111,7 @@ struct BettiLaunch {
     uint32_t* wide_queue;
     // set by launch_betti per launch
     const int32_t* work_list; // null = all complexes 0..num_atoms-1
+    const uint32_t* work_len; // entries of work_list (device)
     uint32_t* queue;          // work counter of this launch
     int32_t skip_above;       // 1 = complexes above NP are left to the overflow launch
     // capacity retry: complexes whose reduction outgrew a kernel's workspace are appended here

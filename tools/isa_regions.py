@@ -1,7 +1,7 @@
 """ISA instruction mix per code region of the narrow Betti kernel (CPU only, no GPU):
 inserts `; MARK_*` asm comments at fixed anchors into a copy of the sources, compiles with
---save-temps and counts instructions between consecutive markers of betti_kernel<48>.
-    python tools/isa_regions.py [outdir]"""
+--save-temps and counts instructions between consecutive markers of betti_kernel<NP>.
+    ISA_NP=44 python tools/isa_regions.py [outdir]"""
 import collections
 import os
 import re
@@ -39,7 +39,8 @@ def main():
                     "-I" + out, "-I" + os.path.join(ROOT, "include"), "--save-temps", "-c", p, "-o",
                     os.path.join(out, "bk.o")], cwd=out, check=True, capture_output=True)
     asm = open(os.path.join(out, "betti_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")).read().split("\n")
-    start = next(i for i, l in enumerate(asm) if l.startswith("_ZN3dgn12betti_kernelILi48EEEvNS_11BettiLaunchE:"))
+    np_ = os.environ.get("ISA_NP", "48")  # instantiation: 32, 44, 48 or 64
+    start = next(i for i, l in enumerate(asm) if l.startswith(f"_ZN3dgn12betti_kernelILi{np_}EEEvNS_11BettiLaunchE:"))
     end = next(i for i in range(start, len(asm)) if asm[i].startswith(".Lfunc_end") )
     region, counts = "ENTRY", collections.defaultdict(collections.Counter)
     for l in asm[start:end]:
@@ -53,10 +54,11 @@ def main():
         op = t[0]
         cls = ("branch" if op.startswith("s_cbranch") or op == "s_branch" else "waitcnt" if op == "s_waitcnt" else
                "salu" if op.startswith("s_") else "lds" if op.startswith("ds_") else
-               "vmem" if op.startswith(("global_", "buffer_", "scratch_", "flat_")) else "valu" if op.startswith("v_") else "other")
+               "scratch" if op.startswith("scratch_") else
+               "vmem" if op.startswith(("global_", "buffer_", "flat_")) else "valu" if op.startswith("v_") else "other")
         counts[region][cls] += 1
     for r, c in counts.items():
-        print(f"{r:14s} " + " ".join(f"{k}={c[k]}" for k in ("valu", "salu", "branch", "lds", "vmem", "waitcnt")))
+        print(f"{r:14s} " + " ".join(f"{k}={c[k]}" for k in ("valu", "salu", "branch", "lds", "vmem", "scratch", "waitcnt")))
     for l in asm:
         if "NumVgprs:" in l or "ScratchSize:" in l:
             pass
