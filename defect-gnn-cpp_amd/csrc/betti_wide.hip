@@ -1160,7 +1160,7 @@ size_t wide_lds_bytes(int nmax) {
 // Scratch layout of one wave for complexes of up to nmax points (all offsets 256-B aligned).
 // big = the capacity-retry layout (complexes whose reduction outgrew the regular caps): column,
 // pivot and pair tables sized for every simplex of the complex, a 16M-entry V store.
-WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit) {
+WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix) {
     WideLayout l{};
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
@@ -1188,7 +1188,7 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit) {
         o = align256(o + bytes);
         return at;
     };
-    l.D = take(4 * n * n);
+    l.D = take(matrix ? 4 * n * n : 0);
     l.mc_e = take(2 * e);
     l.mc_t = take(2 * t);
     l.edges = take(4 * e);
@@ -1196,6 +1196,7 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit) {
     l.na_tau = take(8 * cap);
     l.na_tv = take(8 * cap);
     l.na_col = take(4 * cap);
+    l.na_perm = take(4 * cap);
     l.vstore = take(4 * (int64_t)l.vs_cap);
     l.vlist = take(4 * (int64_t)l.vl_cap);
     l.vdiam = take(4 * (int64_t)l.vl_cap);

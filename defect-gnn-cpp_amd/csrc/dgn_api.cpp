@@ -135,11 +135,13 @@ struct dgn_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int wide_nmax = 0, wide_waves = 0, wide_cap = 0;  // layout the wide scratch's tables were initialised for
+    bool wide_wg = false;                             // ... and whether it is the workgroup kernel's
     // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
     bool dbg_force_retry = false;  // every complex of a Betti pass through the capacity-retry launch
     int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
     int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
+    bool dbg_wide_wg = false;      // workgroup-per-complex kernel for rank-coded 129..362-point complexes (unverified: off)
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
     DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
@@ -457,24 +459,31 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
     WideLayout wl{};
     int wide_waves = 0;
+    // rank-coded wide complexes of 129..362 points (the 10 A path): one workgroup per complex with
+    // the code triangle in LDS (betti_wg.hip); wide_waves then counts workgroups
+    const bool use_wg = c->dbg_wide_wg && c->dbg_wide_c16 && max_points > 64 && max_points <= kC16MaxPoints &&
+                        betti_wg_supported(max_points);
     if (max_points > 64) {
         const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
-        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap);
-        // as many waves as the device keeps resident (dynamic LDS sized by max_points), each
-        // with its own scratch, within half of the free HBM (288 GB per MI355X; at least 8 GB)
+        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap, !use_wg);
+        // as many waves (workgroups) as the device keeps resident (dynamic LDS sized by
+        // max_points), each with its own scratch, within half of the free HBM (288 GB per MI355X;
+        // at least 8 GB)
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
-        const int64_t resident = betti_wide_resident_waves(
-            c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
+        const int64_t resident =
+            use_wg ? betti_wg_resident_blocks(c->device, wide_nmax)
+                   : betti_wide_resident_waves(c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         if (c->dbg_wide_waves > 0 && c->dbg_wide_waves < wide_waves) wide_waves = c->dbg_wide_waves;  // A/B only
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
-        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap) {
+        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap ||
+            c->wide_wg != use_wg) {
             // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
             // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
             // restores both for the entries it used
@@ -482,6 +491,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             c->wide_nmax = wide_nmax;
             c->wide_waves = wide_waves;
             c->wide_cap = wl.na_cap;
+            c->wide_wg = use_wg;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
@@ -571,7 +581,10 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                     wb.rank_codes = codes;
                     wb.rank_sorted = sorted;
                     wb.rank_stride = rstride;
-                    HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
+                    if (use_wg)
+                        HIP_TRY(c, launch_betti_wg(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
+                    else
+                        HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
                 }
                 HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope
             }
@@ -859,6 +872,7 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
         case DGN_DEBUG_WIDE_WAVES: c->dbg_wide_waves = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
         case DGN_DEBUG_WIDE_CAP: c->dbg_wide_cap = value > 0 ? value : 0; return DGN_OK;
+        case DGN_DEBUG_WIDE_WG: c->dbg_wide_wg = value != 0; return DGN_OK;
         default: return fail(c, DGN_ERR_ARG, "dgn_ctx_set_debug: unknown knob " + std::to_string(knob));
     }
 }

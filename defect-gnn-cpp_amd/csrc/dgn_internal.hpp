@@ -137,14 +137,23 @@ struct WideLayout {
     int64_t total;
     int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
-    int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2, d0;
+    int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, na_perm, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2,
+        d0;
 };
 // cap_limit > 0 (tests, DGN_DEBUG_WIDE_CAP): the regular layout's column / pivot / pair tables
 // hold at most cap_limit entries, so ordinary complexes overflow in the kernel and take the
 // capacity-retry path
-WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0);
+// matrix = false: no per-wave distance matrix (the workgroup kernel keeps it in LDS)
+WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0, bool matrix = true);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // device-wide resident waves (occupancy API)
+// workgroup-per-complex kernel (betti_wg.hip) for rank-coded complexes of 129..kC16MaxPoints points:
+// the u16 code triangle and the adjacency in LDS, scratch per workgroup (betti_wide_layout with
+// matrix = false); b.rank_codes / b.rank_sorted required
+bool betti_wg_supported(int nmax);
+size_t betti_wg_lds_bytes(int nmax);
+int betti_wg_resident_blocks(int device, int nmax);
+hipError_t launch_betti_wg(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int blocks);
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
 // occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
 // equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,

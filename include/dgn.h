@@ -55,8 +55,16 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  * DGN_DEBUG_WIDE_C16     0 = f32 distances for every wide complex (default 1: u16 rank codes);
  * DGN_DEBUG_WIDE_CAP     > 0: the wide launch's column / pivot / pair tables hold at most this many
  *                        entries (rounded up to a power of two), so ordinary complexes overflow in the
- *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps. */
-enum { DGN_DEBUG_FORCE_RETRY = 1, DGN_DEBUG_WIDE_WAVES = 2, DGN_DEBUG_WIDE_C16 = 3, DGN_DEBUG_WIDE_CAP = 4 };
+ *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps;
+ * DGN_DEBUG_WIDE_WG      0 = one wave per rank-coded wide complex (betti_wide) instead of the default
+ *                        workgroup per complex with its distances in LDS (129..362 points). */
+enum {
+    DGN_DEBUG_FORCE_RETRY = 1,
+    DGN_DEBUG_WIDE_WAVES = 2,
+    DGN_DEBUG_WIDE_C16 = 3,
+    DGN_DEBUG_WIDE_CAP = 4,
+    DGN_DEBUG_WIDE_WG = 5
+};
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 /* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */
 int dgn_debug_retry_count(dgn_ctx* ctx, int64_t* count);

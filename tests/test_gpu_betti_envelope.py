@@ -1,8 +1,11 @@
 """Envelope of the Betti reduction vs the reference's verbatim vendored Ripser (oracle/_ref), which
 has no workspace caps (third_party/ripser/ripser.cpp:514-1269): complexes whose reduction outgrows
 a kernel's per-wave workspace (cliques: every pairwise distance <= threshold) must be reduced again
-by the capacity-retry launch (betti_wide_kernel, big layout), never fail with DGN_ERR_CAPACITY.
-Counts and (birth, death) pairs bit-exact, compared as sorted multisets."""
+by the capacity-retry launch (betti_wide_kernel, big layout) instead of failing. The big layout has
+caps too (2^24 columns / pivots / pairs / V-store words, betti_wide.hip betti_wide_layout): a
+complex beyond those (e.g. a dense clique above ~465 points, C(n, 3) > 2^24) still returns
+DGN_ERR_CAPACITY; the cases here stay inside them. Counts and (birth, death) pairs bit-exact,
+compared as sorted multisets."""
 
 import numpy as np
 import pytest

@@ -100,3 +100,33 @@ def test_f32_fallback_matches_rank_codes(ctx):
         for d, col in ((0, 0), (1, 2), (2, 3)):
             n = k16[c, col]
             assert np.array_equal(p32[c, d, :n], p16[c, d, :n]), (c, d)
+
+
+WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG
+
+
+def test_workgroup_kernel_matches_wave_kernel(ctx):
+    """The workgroup-per-complex kernel (default for rank-coded 129..362-point complexes, distances
+    in LDS) and the one-wave-per-complex kernel (DGN_DEBUG_WIDE_WG = 0) give the same pairs and
+    counts; both against verbatim Ripser (ripser.cpp:514-1269)."""
+    rng = np.random.default_rng(47)
+    sizes = [340, 200, 131, 90, 362]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.uniform(0, 6.5, size=(n, 3))
+    clouds[1, 100:120] = clouds[1, 0:20]  # exact duplicate points: zero distances and ties
+    npts = np.array(sizes, dtype=np.int32)
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 1)
+    try:
+        _check_clouds(ctx, clouds, npts, 1.8, 16384)
+        pwg, kwg = ctx.host_persistence(clouds, npts, 1.8, cap=16384)
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 0)
+        pw, kw = ctx.host_persistence(clouds, npts, 1.8, cap=16384)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, WG_DEFAULT)
+    assert np.array_equal(kw, kwg)
+    for c in range(len(sizes)):
+        for d, col in ((0, 0), (1, 2), (2, 3)):
+            n = kwg[c, col]
+            a, b = pw[c, d, :n], pwg[c, d, :n]
+            assert np.array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])]), (c, d)

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 B=defect-gnn-cpp_amd/build_var_$TAG
 mkdir -p "$B"
 HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Idefect-gnn-cpp_amd/csrc -Iinclude -mllvm -amdgpu-atomic-optimizer-strategy=DPP $FLAGS"
-for f in graph_kernels betti_kernels betti_wide betti_rank node_kernels; do
+for f in graph_kernels betti_kernels betti_wide betti_wg betti_rank node_kernels; do
   /opt/rocm/bin/hipcc $HF -c defect-gnn-cpp_amd/csrc/$f.hip -o $B/$f.o &
 done
 /opt/rocm/bin/hipcc $HF -x hip -c defect-gnn-cpp_amd/csrc/dgn_api.cpp -o $B/dgn_api.o &
