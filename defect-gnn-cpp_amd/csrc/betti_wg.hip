@@ -130,6 +130,28 @@ struct WgCx {
         return max(max(d(pv(p, 2), pv(p, 1)), d(pv(p, 2), pv(p, 0))), d(pv(p, 1), pv(p, 0)));
     }
     __device__ float value(uint32_t dc) const { return __uint_as_float(vals[dc]); }
+#ifdef DGN_PHASE_TIMING
+    // diagnostics build: wave 0's s_memtime cycles per phase / reduction sub-phase, and counters,
+    // into bl.phase_cycles (the slots tools/diag_wide.py reads)
+    uint64_t tq = 0;
+    __device__ void dg_add(int k, uint64_t v) const {
+        if (wv == 0 && lane == 0 && bl.phase_cycles) atomicAdd(&bl.phase_cycles[k], (unsigned long long)v);
+    }
+    __device__ void dg_mark(int k) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (k >= 0) dg_add(k, t - tq);
+        tq = t;
+    }
+#define WG_MARK(k) dg_mark(k)
+#define WG_COUNT(k, v) dg_add(k, (uint64_t)(v))
+#else
+#define WG_MARK(k) \
+    do {           \
+    } while (0)
+#define WG_COUNT(k, v) \
+    do {               \
+    } while (0)
+#endif
 
     // ---- rank codes -> LDS, threshold code, adjacency bitsets ----
     __device__ void load(int64_t slot) {
@@ -666,6 +688,7 @@ struct WgCx {
     // even: raise the floor and repeat. kInf for the zero column.
     __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
         const int k = lane;
+        WG_COUNT(29, 1);  // pivot searches
         for (;;) {
             uint64_t lmin = kInf, lp = 0;
             int lcnt = 0;
@@ -795,6 +818,7 @@ struct WgCx {
                 if (mq == M) C += wg_ctl.scnt[r][q];
             }
             M = uni64(M);
+            WG_COUNT(30, 1);  // floor rounds
             if (M == kInf) return kInf;
             if (uni(C) & 1u) {
                 tv = uni64(PK);
@@ -810,7 +834,9 @@ struct WgCx {
             err |= kENA;
             return;
         }
+        WG_MARK(-1);
         sort_na(nna);
+        WG_MARK(16);
         const uint64_t* K = sp<uint64_t>(ly.na_key);
         const uint32_t* P = sp<uint32_t>(ly.na_perm);
         const uint64_t* T = sp<uint64_t>(ly.na_tau);
@@ -841,9 +867,12 @@ struct WgCx {
             uint64_t tv = rl64(rv, li);
             const uint32_t cp = rl(rc, li);
             uint32_t app;
+            WG_MARK(21);
             uint64_t meta = lookup(dim, tau, tv, app);
+            WG_MARK(17);
             int v = 0;  // 0 = lazy: V == {this column}
             if (meta != kNoMeta || app != kNone) {
+                WG_COUNT(22, 1);  // columns that need a reduction
                 bool first = true;
                 int64_t guard = 0;
                 for (;;) {
@@ -879,9 +908,14 @@ struct WgCx {
                         err |= kEWork;
                         break;
                     }
+                    WG_MARK(19);
+                    WG_COUNT(24, 1);
+                    WG_COUNT(25, v);
                     tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInf;
+                    WG_MARK(20);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
                     meta = lookup(dim, tau, tv, app);
+                    WG_MARK(17);
                     if (meta == kNoMeta && app == kNone) break;  // tau is this column's pivot
                     if (++guard > ly.guard) {
                         err |= kEGuard;
@@ -909,6 +943,7 @@ struct WgCx {
                 mt = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;
             }
+            WG_MARK(-1);
             // every wave's last lookup of this column reads the table before wave 0 inserts tau (a
             // lagging wave that saw tau's own entry would take another reduction round alone)
             __syncthreads();
@@ -970,7 +1005,9 @@ struct WgCx {
     }
 
     __device__ void run(int64_t gi, int64_t slot, double weight) {
+        WG_MARK(-1);
         load(slot);
+        WG_MARK(0);
         if (threadIdx.x < 4) wg_ctl.ctr[threadIdx.x] = 0u;
         if (wv == 0) {
             prim();
@@ -980,14 +1017,22 @@ struct WgCx {
         }
         __syncthreads();
         const int n_edges = (int)uni((uint32_t)wg_ctl.nedges);
+        WG_MARK(1);
+        WG_COUNT(10, n_edges);
         pass_dim1(n_edges);
         __syncthreads();
+        WG_MARK(2);
+        WG_COUNT(8, uni(wg_ctl.ctr[2]));
         reduce(1, (int)uni(wg_ctl.ctr[2]));
+        WG_MARK(3);
         // reduce ends with a barrier: the clearing marks are complete before the dim-2 pass
         if (err == 0u) {
             pass_dim2(n_edges);
             __syncthreads();
+            WG_MARK(4);
+            WG_COUNT(9, uni(wg_ctl.ctr[3]));
             reduce(2, (int)uni(wg_ctl.ctr[3]));
+            WG_MARK(5);
         } else {
             // no dim-2 pass consumes the clearing marks: erase every triangle entry
             uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
@@ -997,6 +1042,7 @@ struct WgCx {
         }
         if (wv == 0) finish(gi, weight);
         __syncthreads();
+        WG_MARK(6);
     }
 };
 

@@ -90,6 +90,7 @@ struct GraphWork {
     int64_t atoms = -1, structs = -1;
     double rc = 0, eps = 0;
     uint64_t k = 0;
+    int qa = kQA;  // query atoms per count / emit block (graph_tile_atoms)
     uint32_t max_candidates = 0, max_natoms = 0;
     int64_t edges = 0;
     double sum_sq = 0;
@@ -134,6 +135,7 @@ struct dgn_ctx {
     // overflow-tier fork (side stream + events), created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int cus = 0;  // compute units of the device (device_cus)
     int wide_nmax = 0, wide_waves = 0, wide_cap = 0;  // layout the wide scratch's tables were initialised for
     bool wide_wg = false;                             // ... and whether it is the workgroup kernel's
     // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
@@ -279,6 +281,14 @@ int take_flags(dgn_ctx* c) {
     return take_betti_flag(c);
 }
 
+int device_cus(dgn_ctx* c) {
+    if (c->cus <= 0) {
+        hipDeviceProp_t p;
+        c->cus = hipGetDeviceProperties(&p, c->device) == hipSuccess ? p.multiProcessorCount : 256;
+    }
+    return c->cus;
+}
+
 GraphLaunch graph_launch(GraphWork& W, const dgn_batch* b, double rc, double eps, uint64_t kmax, bool use_mask) {
     return GraphLaunch{W.meta.as<StructMeta>(),  W.atom_struct.as<int32_t>(),
                        b->atom_offset,           b->positions,
@@ -286,7 +296,7 @@ GraphLaunch graph_launch(GraphWork& W, const dgn_batch* b, double rc, double eps
                        use_mask ? W.mask.as<uint64_t>() : nullptr,
                        b->num_structures,        b->num_atoms,
                        rc * rc,                  eps,
-                       kmax};
+                       kmax,                     W.qa};
 }
 
 // neighbour counting pass shared by the graph and Betti entry points: prep (geometry, atom map,
@@ -298,7 +308,8 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
                      bool betti = false) {
     GraphWork& W = betti ? c->bw : c->gw;
     const int64_t A = b->num_atoms, B = b->num_structures;
-    const int64_t nblocks = graph_blocks(A);
+    W.qa = graph_tile_atoms(A, device_cus(c));
+    const int64_t nblocks = graph_blocks(A, W.qa);
     const size_t A1 = (size_t)std::max<int64_t>(A, 1);
     HIP_TRY(c, W.meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
     HIP_TRY(c, W.counts.ensure(sizeof(int32_t) * A1));

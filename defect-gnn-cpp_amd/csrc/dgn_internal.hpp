@@ -34,6 +34,7 @@ struct GraphLaunch {
     int64_t num_structures, num_atoms;
     double rc2, eps;
     uint64_t kmax;
+    int32_t qa;                  // query atoms per block of the count / emit (graph_tile_atoms)
 };
 
 struct RbfSpec {
@@ -69,7 +70,15 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
 
 hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out);
 
-inline int64_t graph_blocks(int64_t num_atoms) { return (num_atoms + kQA - 1) / kQA; }
+inline int64_t graph_blocks(int64_t num_atoms, int qa = kQA) { return (num_atoms + qa - 1) / qa; }
+// query atoms per count / emit block: kQA, halved (down to 4) until the launch has >= 8 blocks per
+// CU, so small batches (BASELINE configs 2 and 5) spread one or a few atoms per wave over the chip
+// instead of 16 per wave over a few CUs
+inline int graph_tile_atoms(int64_t num_atoms, int cus) {
+    int qa = kQA;
+    while (qa > 4 && graph_blocks(num_atoms, qa) < 8 * (int64_t)cus) qa >>= 1;
+    return qa;
+}
 int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
 
 // ---- Betti ----

@@ -124,7 +124,7 @@ __device__ __forceinline__ void frac_fixed(const double* R, int k, const double 
 
 // block per structure: atom -> structure map, the far-position check, the per-atom
 // 1/count(species) Betti weight and, for structures above kStage atoms, the cell list
-__global__ __launch_bounds__(256) void prep_atoms_kernel(const StructMeta* __restrict__ meta,
+__global__ __launch_bounds__(1024) void prep_atoms_kernel(const StructMeta* __restrict__ meta,
                                                          const double* __restrict__ pos,
                                                          const int32_t* __restrict__ species,
                                                          int32_t* __restrict__ atom_struct,
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void prep_atoms_kernel(const StructMeta* __res
                                                          uint32_t* __restrict__ error_flag) {
     __shared__ int32_t hist[kCellMax + 1];
     __shared__ int32_t shist[256];
-    __shared__ int32_t part[256 / kWave];
+    __shared__ int32_t part[1024 / kWave];
     const int64_t b = blockIdx.x;
     const int tid = threadIdx.x;
     const StructMeta& sm = meta[b];
@@ -295,10 +295,10 @@ __device__ __forceinline__ StructMeta load_meta_uniform(const StructMeta* p) {
 
 template <class PerAtom>
 __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const StageView st, int64_t a_begin,
-                                                int64_t a_end, int64_t tile, PerAtom&& per_atom) {
+                                                int64_t a_end, int64_t tile, int qa, PerAtom&& per_atom) {
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    const int64_t g0 = a_begin + tile * kQA;
-    const int64_t g1 = g0 + kQA < a_end ? g0 + kQA : a_end;
+    const int64_t g0 = a_begin + tile * qa;
+    const int64_t g1 = g0 + qa < a_end ? g0 + qa : a_end;
     if (g0 >= g1) return;
     const int32_t b_first = uni_i32(g.atom_struct[g0]);
     const int32_t b_last = uni_i32(g.atom_struct[g1 - 1]);
@@ -725,11 +725,12 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     const StageView st = make_stage(stage_mem, kStage, offt_s);
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
-    const int64_t g0 = (int64_t)blockIdx.x * kQA;
+    const int qa = g.qa;
+    const int64_t g0 = (int64_t)blockIdx.x * qa;
     int64_t my_sum = 0;
     uint32_t my_max = 0, my_nat = 0;
     uint64_t my_sq = 0, my_m = 0;
-    for_block_atoms(g, st, 0, g.num_atoms, blockIdx.x, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
+    for_block_atoms(g, st, 0, g.num_atoms, blockIdx.x, qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
         wm[w] = my_m;
     }
     __syncthreads();
-    const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
+    const int nq = (int)(g.num_atoms - g0 < qa ? g.num_atoms - g0 : qa);
     for (int i = threadIdx.x; i < nq; i += kGraphBlock) counts[g0 + i] = cnt_s[i];
     if (mask_out)
         for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock) {
@@ -1295,8 +1296,9 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     const int64_t x = blockIdx.x;
     const bool is_rbf = x < 2 * both ? (x & 1) != 0 : tl.nrbf > tl.nrow;
     const int64_t tile = (is_rbf ? tl.rbf0 : tl.row0) + (x < 2 * both ? x >> 1 : x - both);
-    const int64_t g0 = tile * kQA;
-    const int nq = (int)(g.num_atoms - g0 < kQA ? g.num_atoms - g0 : kQA);
+    const int qa = g.qa;
+    const int64_t g0 = tile * qa;
+    const int nq = (int)(g.num_atoms - g0 < qa ? g.num_atoms - g0 : qa);
 #ifdef DGN_EMIT_PHASES
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tprev = __builtin_amdgcn_s_memtime();
@@ -1347,15 +1349,16 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         }
     }
 
-    // local scan of this block's counts -> row starts (and row_ptr); kQA == one wave
+    // local scan of this block's counts -> row starts (and row_ptr); qa <= kQA == one wave
     if (w == 0) {
         const int64_t gi = g0 + lane;
-        const int64_t c = gi < g.num_atoms ? min(counts[gi], K) : 0;  // kept rows: min(m, max_neighbors)
+        const bool mine = lane < qa && gi < g.num_atoms;
+        const int64_t c = mine ? min(counts[gi], K) : 0;  // kept rows: min(m, max_neighbors)
         const int64_t inc = wave_inclusive_sum(c);
         const int64_t start = block_offsets[tile] + inc - c;
         row_start[lane] = start;
         if (lane == kWave - 1) row_start[kQA] = start + c;
-        if (gi < g.num_atoms) {
+        if (mine) {
             row_ptr[gi] = start;
             if (gi == g.num_atoms - 1) row_ptr[g.num_atoms] = start + c;
         }
@@ -1371,7 +1374,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     DGN_LDS double* kd = key_d + w * CAP;
     DGN_LDS uint64_t* kj = key_j + w * CAP;
     DGN_LDS double* sd = sorted_d + w * (CAP + 1);
-    for_block_atoms(g, st, 0, g.num_atoms, tile, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
+    for_block_atoms(g, st, 0, g.num_atoms, tile, qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
                                                __attribute__((always_inline)) {
         EMIT_STAMP(1);
         const int li = (int)(gi - M.first);
@@ -1533,7 +1536,7 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
             mask_s[x / kMaskWords][x % kMaskWords] = g.mask[g0 * kMaskWords + x];
         __syncthreads();
     }
-    for_block_atoms(g, st, first, first + count, blockIdx.x, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {
+    for_block_atoms(g, st, first, first + count, blockIdx.x, kQA, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         const int64_t c = gi - first;
         double q[3];
@@ -1666,14 +1669,17 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
     if (B <= 0) return hipSuccess;
     hipLaunchKernelGGL(prep_meta_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s, lattice, atom_offset, B,
                        rc, meta);
-    hipLaunchKernelGGL(prep_atoms_kernel, dim3((unsigned)B), dim3(256), 0, s, meta, pos, species, atom_struct,
+    // block per structure; small batches (a few large cells, e.g. BASELINE config 5's supercell)
+    // get 1024 threads per block for the cell-list sort
+    const unsigned threads = B < 512 ? 1024u : 256u;
+    hipLaunchKernelGGL(prep_atoms_kernel, dim3((unsigned)B), dim3(threads), 0, s, meta, pos, species, atom_struct,
                        cell_start, cell_pos, weight, error_flag);
     return hipGetLastError();
 }
 
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
                               uint64_t* block_aux, uint64_t* mask_out) {
-    const int64_t nb = graph_blocks(g.num_atoms);
+    const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
     hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
                        block_aux, mask_out);
@@ -1701,7 +1707,7 @@ template <int CAP, bool STREAM>
 static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const int32_t* counts,
                           const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
                           void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
-    const int64_t nt = graph_blocks(g.num_atoms);
+    const int64_t nt = graph_blocks(g.num_atoms, g.qa);
     const int nwm = (stage + 63) / 64;
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
     const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
@@ -1769,7 +1775,7 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
-    const int64_t nb = graph_blocks(g.num_atoms);
+    const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
 #ifdef DGN_EMIT_FLAT
     const bool stream = false;  // A/B diagnostics: per-atom write_rbf_flat

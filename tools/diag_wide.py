@@ -13,6 +13,8 @@ import dgn  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 ctx = dgn.Context(0)
+if os.environ.get("DGN_WIDE_WG"):
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, int(os.environ["DGN_WIDE_WG"]))
 batch = dgn.synth_batch("fcc", 4, B)
 A = batch["positions"].shape[0]
 t0 = time.perf_counter()
@@ -28,7 +30,7 @@ print(json.dumps({"complexes": A, "s": round(dt, 3), "cycles_per_complex": round
                   "edges": ph[10] / A, "na1": ph[8] / A, "na2": ph[9] / A,
                   "reduce_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(
                       ["sort", "hfind", "apparent_owner", "toggles", "pivot_of_V", "finalize"])},
-                  "adds_per_complex": ph[24] / A,
+                  "adds_per_complex": ph[24] / A, "reduced_columns_per_complex": ph[22] / A,
                   "dim2_walk": {"columns_walked": ph[28] / A, "mean_steps": ph[26] / max(ph[28], 1),
                                 "wave_iterations_per_complex": ph[27] / A,
                                 "lane_efficiency": ph[26] / max(64 * ph[27], 1)}, "mean_V_per_pivot_search": ph[25] / max(ph[24], 1),
