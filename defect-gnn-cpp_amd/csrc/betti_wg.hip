@@ -8,18 +8,23 @@
 // overflow L2 and the Infinity Cache, and every walk step waits for HBM. Here the
 // complex's u16 rank codes (betti_rank_codes: order- and equality-preserving, C(362, 2) < 2^16)
 // sit in LDS as the packed lower triangle (<= 128 KB) next to the adjacency bitsets (<= 17 KB),
-// so every distance read of the walks and of the pivot searches is an LDS read, and the
-// workgroup's waves share the work:
-//   * load, adjacency: all waves;  Prim (wave 0) beside the edge list (wave 1);
-//   * dim-1 / dim-2 apparent passes: lane per column, the columns dealt to the waves from LDS
-//     counters (dim 2: a per-lane work queue over the edges, as betti_wide.hip);
-//   * the non-apparent columns: bitonic-sorted in scratch by all threads;
-//   * the reduction, column by column in Ripser's order: every wave follows the same control
-//     flow (the same uniform values from the same reads); the V list lives in LDS and only wave 0
-//     changes it; the pivot search — the reduction's hot loop — deals its (V entry, bitset word)
-//     pairs to the waves and combines their minima through LDS (one barrier per floor round);
-//     scratch writes (pivot table, V store, pairs, clearing marks) are wave 0's, published by the
-//     barrier that ends the column.
+// so every distance read is an LDS read, and no per-simplex table lives in memory at all:
+//   * load, adjacency: all waves;  Prim: wave 0;
+//   * dim-1 / dim-2 apparent passes: lane per column, the edges dealt to the lanes as (row, bitset
+//     word) units of the LDS adjacency from an LDS counter — no edge list in memory (dim 2: a
+//     per-lane work queue over the edges' triangles, as betti_wide.hip). No min-cofacet
+//     tables: the reduction re-derives an apparent owner from the LDS matrix when it needs one
+//     (lane-parallel, a few hundred cycles instead of a scattered HBM read);
+//   * clearing: the dim-1 pivots (apparent and reduced) set a bit per triangle in a scratch bitset;
+//     the dim-2 pass does not consult it (a cleared triangle is a dim-1 death, so never apparent in
+//     dim 2 — each simplex is in at most one persistence pair) and the cleared columns are dropped
+//     from the dim-2 column list before the sort, then the listed bits are reset;
+//   * the reduction, in Ripser's column order, is driven by wave 0 alone (column records, pivot
+//     table, V list in LDS, V store); the other waves sleep at a barrier and wake only for the pivot
+//     searches — the reduction's hot loop — whose (V entry, bitset word) pairs they share, their
+//     minima combined through LDS (two barriers per floor round, none per column);
+//   * the pivot table (scratch) is sized by the column count, so it stays cache-resident, and an
+//     insert reuses the empty slot its last lookup found.
 // Same algorithm and output contract as betti_wide.hip (pairing of a total order: the emitted
 // multiset equals Ripser's, ripser.cpp:514-1269; death > birth only, essential dim >= 1 classes
 // not emitted, ripser.cpp:1209-1225, 1240). Capacity overflows list the complex for the
@@ -40,8 +45,6 @@ constexpr int kWgThreads = kNW * kWave;
 constexpr int kVlCap = 512;                // V list entries (LDS); more: capacity retry
 constexpr uint64_t kInf = ~0ull;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint16_t kMcNone = 0xFFFF;     // not a column, or no cofacet
-constexpr uint16_t kMcCleared = 0xFFFE;  // triangle is the pivot of a dim-1 column (clearing)
 constexpr uint64_t kLazy = 1ull << 63;    // pivot meta: V = {column simplex}
 constexpr uint64_t kNoMeta = ~0ull;
 constexpr int kMetaLenBits = 24;
@@ -54,24 +57,24 @@ constexpr uint64_t VM = (1ull << VB) - 1;
 
 // control block (static LDS)
 struct WgCtl {
-    uint32_t ticket[2];             // complex dequeue (double-buffered by iteration parity)
-    uint32_t ctr[4];                // pass counters: dim-1 edges, dim-2 edges, dim-1 / dim-2 columns
-    int32_t nedges;
-    uint32_t cnt;                   // threshold search
-    int32_t vv[2];                  // V length after wave 0's toggles (double-buffered by round)
-    uint32_t vok[2];
-    uint64_t smin[2][kNW];          // pivot search: per-wave minimum, multiplicity, packed cofacet
-    uint64_t spk[2][kNW];
-    uint32_t scnt[2][kNW];
-    uint32_t vl[kVlCap];            // V list (packed simplices) and their diameters
+    uint32_t ticket[2];  // complex dequeue (double-buffered by iteration parity)
+    uint32_t ctr[6];     // dim-1 / dim-2 edge units, dim-1 / dim-2 columns, clear list
+    uint32_t err;        // wave 0's error bits after a reduction
+    // pivot-search request (wave 0 -> helper waves) and the per-wave results
+    uint64_t rq_floor;
+    int32_t rq_v, rq_dim, rq_stop, npiv;
+    uint64_t smin[kNW];
+    uint64_t spk[kNW];
+    uint32_t scnt[kNW];
+    uint32_t vl[kVlCap];  // V list (packed simplices) and their diameters
     uint32_t vd[kVlCap];
 };
 __shared__ WgCtl wg_ctl;
 extern __shared__ uint64_t wg_dyn[];
 
-__device__ __forceinline__ uint64_t bin2(uint64_t v) { return v * (v - 1) / 2; }
-__device__ __forceinline__ uint64_t bin3(uint64_t v) { return v * (v - 1) * (v - 2) / 6; }
-__device__ __forceinline__ uint64_t bin4(uint64_t v) { return v * (v - 1) * (v - 2) * (v - 3) / 24; }
+__device__ __forceinline__ uint32_t b2(uint32_t v) { return v * (v - 1u) / 2u; }
+__device__ __forceinline__ uint32_t b3(uint32_t v) { return b2(v) * (v - 2u) / 3u; }
+__device__ __forceinline__ uint32_t b4(uint32_t v) { return b3(v) * (v - 3u) / 4u; }  // < 2^32 for v <= 362
 __device__ __forceinline__ uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
 __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
     return ((uint64_t)rl((uint32_t)(x >> 32), l) << 32) | rl((uint32_t)x, l);
@@ -79,10 +82,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t x, int l) {
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
 __device__ __forceinline__ int pv(uint64_t p, int field) { return (int)((p >> (VB * field)) & VM); }
-__device__ __forceinline__ uint64_t pidx(int nv, uint64_t p) {
-    if (nv == 2) return bin2(pv(p, 1)) + pv(p, 0);
-    if (nv == 3) return bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
-    return bin4(pv(p, 3)) + bin3(pv(p, 2)) + bin2(pv(p, 1)) + pv(p, 0);
+// combinatorial index (Ripser's colex numbering, ripser.cpp:181-201), 32-bit: C(362, 4) < 2^32
+__device__ __forceinline__ uint32_t pidx(int nv, uint64_t p) {
+    if (nv == 2) return b2(pv(p, 1)) + pv(p, 0);
+    if (nv == 3) return b3(pv(p, 2)) + b2(pv(p, 1)) + pv(p, 0);
+    return b4(pv(p, 3)) + b3(pv(p, 2)) + b2(pv(p, 1)) + pv(p, 0);
 }
 __device__ __forceinline__ uint64_t pinsert(int nv, uint64_t p, int x) {
     int below = 0;
@@ -91,7 +95,8 @@ __device__ __forceinline__ uint64_t pinsert(int nv, uint64_t p, int x) {
     return ((p & ~mask) << VB) | ((uint64_t)x << (VB * below)) | (p & mask);
 }
 // key: (distance code << 32) | ~index — ascending keys are Ripser's filtration order
-__device__ __forceinline__ uint64_t wkey(uint32_t dc, uint64_t idx) { return ((uint64_t)dc << 32) | (~idx & 0xFFFFFFFFull); }
+// (greater_diameter_or_smaller_index, ripser.cpp:318-324)
+__device__ __forceinline__ uint64_t wkey(uint32_t dc, uint32_t idx) { return ((uint64_t)dc << 32) | (uint64_t)(~idx); }
 __device__ __forceinline__ uint32_t kdiam(uint64_t key) { return (uint32_t)(key >> 32); }
 __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 // workgroup-scope LDS add of `v` by lane 0 (every lane executes the atomic: no branch on the
@@ -99,6 +104,22 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 __device__ __forceinline__ uint32_t lds_add_uniform(uint32_t* p, uint32_t v) {
     const uint32_t old = __hip_atomic_fetch_add(p, lane_id() == 0 ? v : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return rl(old, 0);
+}
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt), not
+// for its outstanding global loads and stores as __syncthreads' workgroup fence does (vmcnt(0):
+// wave 0's table inserts and V-store writes would stall every pivot-search round)
+__device__ __forceinline__ void sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+// min over the wave of a u32 (DPP row rotations + 4 readlanes)
+__device__ __forceinline__ uint32_t wave_min32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x121, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x122, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x124, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x128, 0xf, 0xf, false));
+    return min(min(rl(x, 0), rl(x, 16)), min(rl(x, 32), rl(x, 48)));
 }
 
 template <int KW>
@@ -114,8 +135,9 @@ struct WgCx {
     bool zero0;            // code 0 is the distance 0
     uint32_t err;
     int n_d0, n_inf0, n_p1, n_p2;
-    uint32_t rnd;          // LDS publish rounds (slot parity), identical in every wave
     const uint32_t* vals;  // the complex's sorted f32 distances (code -> value)
+    uint32_t hmask;        // pivot table slots in use - 1 (sized per reduction)
+    int ins_slot;          // the empty table slot the last lookup found (-1: probe on insert)
 
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
@@ -129,7 +151,6 @@ struct WgCx {
         if (dim == 1) return d(pv(p, 1), pv(p, 0));
         return max(max(d(pv(p, 2), pv(p, 1)), d(pv(p, 2), pv(p, 0))), d(pv(p, 1), pv(p, 0)));
     }
-    __device__ float value(uint32_t dc) const { return __uint_as_float(vals[dc]); }
 #ifdef DGN_PHASE_TIMING
     // diagnostics build: wave 0's s_memtime cycles per phase / reduction sub-phase, and counters,
     // into bl.phase_cycles (the slots tools/diag_wide.py reads)
@@ -170,7 +191,8 @@ struct WgCx {
             }
         }
         // ub = #{sorted distances <= thr} (sparse_distance_matrix keeps d <= threshold,
-        // ripser.cpp:386-395): two rounds of 512 parallel probes of the sorted triangle
+        // ripser.cpp:386-395): two rounds of parallel probes of the sorted triangle (m >= 2016
+        // for the > 64-point complexes of the wide list, so every first-round probe is >= 0)
         const uint32_t tb = __float_as_uint(bl.thr);
         const int64_t pr = ((int64_t)(tid + 1) * m) / kWgThreads - 1;
         const int k1 = __syncthreads_count(pr >= 0 && vals[pr] <= tb);
@@ -202,7 +224,7 @@ struct WgCx {
             const int v = 64 * t + lane;
             best[t] = kInf;
             bp[t] = 0;
-            if (t < W && v < n && v != 0 && ((aw(0, t) >> lane) & 1ull)) best[t] = wkey(d(0, v), bin2(v));
+            if (t < W && v < n && v != 0 && ((aw(0, t) >> lane) & 1ull)) best[t] = wkey(d(0, v), b2(v));
         }
         n_inf0 = 1;
         n_d0 = 0;
@@ -241,7 +263,7 @@ struct WgCx {
             for (int t = 0; t < KW; ++t) {
                 const int w = 64 * t + lane;
                 if (t < W && w < n && !((intree >> t) & 1u) && ((aw(v, t) >> lane) & 1ull)) {
-                    const uint64_t k = wkey(d(v, w), v > w ? bin2(v) + w : bin2(w) + v);
+                    const uint64_t k = wkey(d(v, w), v > w ? b2(v) + w : b2(w) + v);
                     if (k < best[t]) {
                         best[t] = k;
                         bp[t] = v;
@@ -251,19 +273,46 @@ struct WgCx {
         }
     }
 
-    // ---- edges (i > j, d <= thr) in index order (wave 1) ----
-    __device__ int edge_list() {
-        uint32_t* edges = sp<uint32_t>(ly.edges);
-        int off = 0;
-        for (int i = 1; i < n; ++i)
-            for (int w = 0; 64 * w < i; ++w) {
-                uint64_t bits = aw(i, w);
-                const int lim = i - 64 * w;
-                if (lim < 64) bits &= (1ull << lim) - 1ull;
-                if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = ((uint32_t)i << VB) | (uint32_t)(64 * w + lane);
-                off += __popcll(bits);
+    // ---- edge source of the lane-parallel passes: units (row i, bitset word w), u = i W + w,
+    // dealt from an LDS counter; a unit holds the edges (i, j), j < i, of word w (read from the LDS
+    // adjacency: no edge list in memory). Lanes with no edge left take new units together. ----
+    struct EdgeSrc {
+        int ui = 0;         // current unit's row
+        int uw = 0;         // current unit's word
+        uint64_t ub = 0;    // its remaining j bits
+        bool drained = false;
+    };
+    // every lane without edges left gets a unit with at least one edge, or the counter is drained
+    __device__ void units_refill(EdgeSrc& es, uint32_t* ctr, bool want) const {
+        for (;;) {
+            const bool need = want && es.ub == 0ull && !es.drained;
+            const uint64_t bal = ballot(need);
+            if (!bal) return;
+            const uint32_t base = lds_add_uniform(ctr, (uint32_t)__popcll(bal));
+            if (need) {
+                const int u = (int)(base + (uint32_t)mask_prefix(bal));
+                if (u >= n * W) {
+                    es.drained = true;
+                } else {
+                    const int i = u / W, w = u - i * W;
+                    uint64_t bits = 64 * w < i ? aw(i, w) : 0ull;
+                    const int lim = i - 64 * w;
+                    if (lim < 64) bits &= (1ull << (lim > 0 ? lim : 0)) - 1ull;
+                    es.ui = i;
+                    es.uw = w;
+                    es.ub = bits;
+                }
             }
-        return off;
+        }
+    }
+    // the lane's next edge (i > j) from its unit; false when the lane has none
+    __device__ bool units_next(EdgeSrc& es, int& i, int& j) const {
+        if (es.ub == 0ull) return false;
+        const int bit = __ffsll((unsigned long long)es.ub) - 1;
+        es.ub &= es.ub - 1ull;
+        i = es.ui;
+        j = 64 * es.uw + bit;
+        return true;
     }
 
     // append the lanes' non-apparent columns (lanes with `na`) through the LDS column counter
@@ -281,80 +330,85 @@ struct WgCx {
             }
         }
     }
+    // clearing (dim-1 pivot triangles): a bit per triangle index in the bitset (layout mc_t), each
+    // set bit's word listed (layout mc_e) for the reset at the end of the complex
+    __device__ void clear_mark(bool on, uint32_t tidx) {
+        const uint64_t bal = ballot(on);
+        if (!bal) return;
+        const uint32_t base = lds_add_uniform(&wg_ctl.ctr[4], (uint32_t)__popcll(bal));
+        if (on) {
+            atomicOr(sp<uint32_t>(ly.mc_t) + (tidx >> 5), 1u << (tidx & 31));
+            sp<uint32_t>(ly.mc_e)[base + (uint32_t)mask_prefix(bal)] = tidx >> 5;
+        }
+    }
 
-    // ---- dim 1: lane per column (non-tree edge), 64-edge chunks dealt from an LDS counter ----
-    __device__ void pass_dim1(int n_edges) {
-        const uint32_t* edges = sp<uint32_t>(ly.edges);
-        uint16_t* mc_e = sp<uint16_t>(ly.mc_e);
-        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+    // ---- dim 1: lane per column (non-tree edge), edges from the LDS units ----
+    __device__ void pass_dim1() {
+        EdgeSrc es;
         for (;;) {
-            const int base = (int)lds_add_uniform(&wg_ctl.ctr[0], kWave);
-            if (base >= n_edges) break;
-            const int e = base + lane;
-            bool na = false;
+            units_refill(es, &wg_ctl.ctr[0], true);
+            int i = 0, j = 0;
+            const bool have = units_next(es, i, j);
+            if (!ballot(have)) break;
+            bool na = false, app = false;
             uint64_t colkey = 0, best = kInf, bestp = 0;
             uint32_t colp = 0;
-            if (e < n_edges) {
-                const uint32_t ed = edges[e];
-                const int i = (int)(ed >> VB), j = (int)(ed & VM);
-                uint16_t mc = kMcNone;
-                if (!is_tree(i, j)) {
-                    const uint32_t dij = d(i, j);
-                    colp = ed;
-                    colkey = wkey(dij, bin2(i) + j);
-                    // F-minimal cofacet: walking k downwards over the common neighbours, the
-                    // first k with both distances <= d(i, j) ends the walk; before it, a smaller k
-                    // wins only with a strictly smaller diameter
-                    uint32_t bd = 0xFFFFFFFFu, hda = 0, hdb = 0;
-                    int bk = -1;
-                    bool found = false;
-                    for (int w = W - 1; w >= 0 && !found; --w) {
-                        uint64_t m = aw(i, w) & aw(j, w);
-                        while (m != 0ull && !found) {
-                            const int bit = 63 - __clzll((long long)m);
-                            m &= ~(1ull << bit);
-                            const int k = 64 * w + bit;
-                            const uint32_t da = d(i, k), db = d(j, k);
-                            const uint32_t dk = max(da, db);
-                            if (dk <= dij) {
-                                bd = dij;
-                                bk = k;
-                                found = true;
-                                hda = da;
-                                hdb = db;
-                            } else if (dk < bd) {
-                                bd = dk;
-                                bk = k;
-                            }
+            if (have && !is_tree(i, j)) {
+                const uint32_t ed = ((uint32_t)i << VB) | (uint32_t)j;
+                const uint32_t dij = d(i, j);
+                colp = ed;
+                colkey = wkey(dij, b2(i) + j);
+                // F-minimal cofacet: walking k downwards over the common neighbours, the first k
+                // with both distances <= d(i, j) ends the walk; before it, a smaller k wins only
+                // with a strictly smaller diameter
+                uint32_t bd = 0xFFFFFFFFu, hda = 0, hdb = 0;
+                int bk = -1;
+                bool found = false;
+                for (int w = W - 1; w >= 0 && !found; --w) {
+                    uint64_t m = aw(i, w) & aw(j, w);
+                    while (m != 0ull && !found) {
+                        const int bit = 63 - __clzll((long long)m);
+                        m &= ~(1ull << bit);
+                        const int k = 64 * w + bit;
+                        const uint32_t da = d(i, k), db = d(j, k);
+                        const uint32_t dk = max(da, db);
+                        if (dk <= dij) {
+                            bd = dij;
+                            bk = k;
+                            found = true;
+                            hda = da;
+                            hdb = db;
+                        } else if (dk < bd) {
+                            bd = dk;
+                            bk = k;
                         }
                     }
-                    if (bk >= 0) {
-                        bestp = pinsert(2, ed, bk);
-                        best = wkey(bd, pidx(3, bestp));
-                        // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet
-                        const bool app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
-                        if (app) mc_t[pidx(3, bestp)] = kMcCleared;  // clearing for dim 2
-                        else na = true;
-                        mc = (uint16_t)bk;
-                    }
                 }
-                mc_e[bin2(i) + j] = mc;
+                if (bk >= 0) {
+                    bestp = pinsert(2, ed, bk);
+                    best = wkey(bd, pidx(3, bestp));
+                    // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet
+                    app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
+                    na = !app;
+                }
             }
+            clear_mark(app, app ? pidx(3, bestp) : 0u);  // clearing for dim 2
             na_append(na, &wg_ctl.ctr[2], colkey, best, bestp, colp);
         }
     }
 
-    // ---- dim 2: lane per column (uncleared triangle), a per-lane work queue over the edges,
-    // edges dealt from an LDS counter (see betti_wide.hip pass_dim2) ----
+    // ---- dim 2: lane per column (triangle), a per-lane work queue over the edges, edges dealt
+    // from an LDS counter (see betti_wide.hip pass_dim2). Cleared triangles are walked too (they are
+    // never apparent) and dropped from the column list by the sort's filter ----
     static constexpr int kStep = 4;
-    __device__ void pass_dim2(int n_edges) {
-        const uint32_t* edges = sp<uint32_t>(ly.edges);
-        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+    __device__ void pass_dim2() {
+        EdgeSrc es;
         int ea = 0, eb = 0, tw = -1;
         uint64_t tm = 0;
-        bool act = false, fresh = false, drained = false;
+        bool act = false, fresh = false;
         int c = 0, w = 0, bk = 0;
-        uint64_t m = 0, tidx = 0;
+        uint64_t m = 0;
+        uint32_t tidx = 0;
         uint32_t bd = 0xFFFFFFFFu;
         uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, colp = 0, hda = 0, hdb = 0, hdc = 0;
         bool found = false;
@@ -371,18 +425,12 @@ struct WgCx {
                     if (lim < 64) tm &= (1ull << lim) - 1ull;
                 }
                 const bool need = !act && tm == 0ull;
-                const uint64_t bal = ballot(need);
-                if (!bal || drained) break;
-                const int base = (int)lds_add_uniform(&wg_ctl.ctr[1], (uint32_t)__popcll(bal));
-                if (base >= n_edges) {
-                    drained = true;
-                    break;
-                }
-                const int e = base + mask_prefix(bal);
-                if (need && e < n_edges) {
-                    const uint32_t ed = edges[e];
-                    ea = (int)(ed >> VB);
-                    eb = (int)(ed & VM);
+                if (!ballot(need && (es.ub != 0ull || !es.drained))) break;
+                units_refill(es, &wg_ctl.ctr[1], need);
+                int i = 0, j = 0;
+                if (need && units_next(es, i, j)) {
+                    ea = i;
+                    eb = j;
                     tw = 0;
                     tm = aw(ea, 0) & aw(eb, 0);
                     if (eb < 64) tm &= (1ull << eb) - 1ull;
@@ -392,7 +440,7 @@ struct WgCx {
                 c = 64 * tw + __ffsll((unsigned long long)tm) - 1;
                 tm &= tm - 1ull;
                 act = fresh = true;
-                tidx = bin3(ea) + bin2(eb) + c;
+                tidx = b3(ea) + b2(eb) + c;
                 colp = ((uint32_t)ea << (2 * VB)) | ((uint32_t)eb << VB) | (uint32_t)c;
                 w = W - 1;
                 m = aw(ea, w) & aw(eb, w) & aw(c, w);
@@ -427,77 +475,89 @@ struct WgCx {
                     dbv[j] = d(b, k);
                     dc[j] = d(c, k);
                 }
-                bool cleared = false;
                 if (fresh) {
-                    cleared = mc_t[tidx] == kMcCleared;
                     dab = d(a, b);
                     dac = d(a, c);
                     dbc = d(b, c);
                     ds = max(max(dab, dac), dbc);
                     fresh = false;
                 }
-                bool done;
-                if (cleared) {
-                    mc_t[tidx] = kMcNone;  // consumed: the entry leaves the complex non-cleared
-                    done = true;
-                } else {
 #pragma unroll
-                    for (int j = 0; j < kStep; ++j) {
-                        if (!val[j] || found) continue;
-                        const int k = kk[j];
-                        const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
-                        if (dk <= ds) {
-                            bd = ds;
-                            bk = k;
-                            found = true;
-                            hda = da[j];
-                            hdb = dbv[j];
-                            hdc = dc[j];
-                        } else if (dk < bd) {
-                            bd = dk;
-                            bk = k;
-                        }
+                for (int j = 0; j < kStep; ++j) {
+                    if (!val[j] || found) continue;
+                    const int k = kk[j];
+                    const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
+                    if (dk <= ds) {
+                        bd = ds;
+                        bk = k;
+                        found = true;
+                        hda = da[j];
+                        hdb = dbv[j];
+                        hdc = dc[j];
+                    } else if (dk < bd) {
+                        bd = dk;
+                        bk = k;
                     }
-                    done = found || !val[kStep - 1];
-                    if (done) {
-                        uint16_t mc = kMcNone;
-                        uint64_t best = kInf, bestp = 0;
-                        if (bk >= 0) {
-                            bestp = pinsert(3, colp, bk);
-                            best = wkey(bd, pidx(4, bestp));
-                            const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
-                                             (bk > b || max(max(hda, hdc), dac) < ds) &&
-                                             (bk > c || max(max(hda, hdb), dab) < ds);
-                            na = !app;
-                            mc = (uint16_t)bk;
-                        }
-                        mc_t[tidx] = mc;
+                }
+                if (found || !val[kStep - 1]) {
+                    if (bk >= 0) {  // no cofacet: zero coboundary, not a column
+                        const uint64_t bestp = pinsert(3, colp, bk);
+                        const bool app = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
+                                         (bk > b || max(max(hda, hdc), dac) < ds) &&
+                                         (bk > c || max(max(hda, hdb), dab) < ds);
+                        na = !app;
                         colkey = wkey(ds, tidx);
-                        ntau = best;
+                        ntau = wkey(bd, pidx(4, bestp));
                         ntv = bestp;
                         ncolp = colp;
                     }
+                    act = false;
                 }
-                if (done) act = false;
             }
             na_append(na, &wg_ctl.ctr[3], colkey, ntau, ntv, ncolp);
         }
     }
 
+    // sum of one int per thread over the workgroup (LDS: the pivot-search result slots)
+    __device__ int block_sum(int x) {
+        const int s = wave_sum(x);
+        if (lane == 0) wg_ctl.scnt[wv] = (uint32_t)s;
+        __syncthreads();
+        int t = 0;
+#pragma unroll
+        for (int q = 0; q < kNW; ++q) t += (int)wg_ctl.scnt[q];
+        __syncthreads();
+        return (int)uni((uint32_t)t);
+    }
+
     // ---- non-apparent columns in Ripser's order: bitonic sort (key descending) of (key, slot)
-    // pairs in scratch by all threads; 4 compare-exchanges per thread per step with their loads
-    // issued together ----
-    __device__ void sort_na(int cnt) {
+    // pairs in scratch by all threads, 4 compare-exchanges per thread per step with their loads
+    // issued together; dim 2 first drops the cleared columns (key 0 sorts last, like the
+    // padding). Returns the number of columns to reduce. ----
+    __device__ int sort_na(int dim, int cnt) {
         const int tid = threadIdx.x;
         int N = 1;
         while (N < cnt) N <<= 1;
         uint64_t* K = sp<uint64_t>(ly.na_key);
         uint32_t* P = sp<uint32_t>(ly.na_perm);
+        const uint32_t* Cc = sp<uint32_t>(ly.na_col);
+        const uint32_t* clr = sp<uint32_t>(ly.mc_t);
+        int drop = 0;
         for (int i = tid; i < N; i += kWgThreads) {
-            if (i >= cnt) K[i] = 0ull;  // padding sorts last
+            bool gone = i >= cnt;
+            if (dim == 2 && !gone) {
+                const uint32_t cp = Cc[i];
+                const uint32_t t = b3(cp >> (2 * VB)) + b2((cp >> VB) & VM) + (cp & VM);
+                // the bits were set by L2 atomics: an L1-bypassing (agent-scope) load
+                const uint32_t word = __hip_atomic_load(clr + (t >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                gone = (word >> (t & 31)) & 1u;
+                drop += gone ? 1 : 0;
+            }
+            if (gone) K[i] = 0ull;
             P[i] = (uint32_t)i;
         }
-        __syncthreads();
+        const int dropped = dim == 2 ? block_sum(drop) : 0;
+        if (dim != 2) __syncthreads();
         const int half = N >> 1;
         for (int k = 2; k <= N; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -530,101 +590,108 @@ struct WgCx {
                 }
                 __syncthreads();
             }
+        return cnt - dropped;
     }
 
-    // ---- pivot table: open addressing in scratch (key 0 = empty), written by wave 0 ----
+    // ---- pivot table: open addressing in scratch (key 0 = empty), wave 0 only ----
     __device__ static uint32_t hmix(uint64_t k) {
         k ^= k >> 33;
         k *= 0xff51afd7ed558ccdull;
         k ^= k >> 33;
         return (uint32_t)k;
     }
-    __device__ uint64_t hfind(uint64_t k) const {
+    __device__ uint64_t hfind(uint64_t k) {
         const uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint64_t* HM = sp<uint64_t>(ly.h_meta);
-        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
-        const uint32_t base = hmix(k) & mask;
-        for (int probe = 0; probe < ly.h_cap; probe += kWave) {
-            const uint64_t x = HK[(base + (uint32_t)(probe + lane)) & mask];
+        const uint32_t base = hmix(k) & hmask;
+        for (uint32_t probe = 0; probe <= hmask; probe += kWave) {
+            const uint64_t x = HK[(base + probe + (uint32_t)lane) & hmask];
             const uint64_t hit = ballot(x == k), emp = ballot(x == 0ull);
             const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
             const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
-            if (fh < fe) return uni64(HM[(base + (uint32_t)(probe + fh)) & mask]);
-            if (fe < kWave) return kNoMeta;
+            if (fh < fe) return uni64(HM[(base + probe + (uint32_t)fh) & hmask]);
+            if (fe < kWave) {
+                ins_slot = (int)((base + probe + (uint32_t)fe) & hmask);
+                return kNoMeta;
+            }
         }
+        ins_slot = -1;
         return kNoMeta;
     }
-    // wave 0 writes; every wave gets the same answer (the table has 2 na_cap slots)
     __device__ bool hinsert(uint64_t k, uint64_t meta, int npiv) {
         if (npiv >= ly.na_cap) return false;
-        if (wv != 0) return true;
         uint64_t* HK = sp<uint64_t>(ly.h_key);
         uint64_t* HM = sp<uint64_t>(ly.h_meta);
-        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
-        const uint32_t base = hmix(k) & mask;
-        for (int probe = 0; probe < ly.h_cap; probe += kWave) {
-            const uint64_t x = HK[(base + (uint32_t)(probe + lane)) & mask];
-            const uint64_t emp = ballot(x == 0ull);
-            if (emp) {
-                const uint32_t slot = (base + (uint32_t)(probe + __ffsll((unsigned long long)emp) - 1)) & mask;
-                if (lane == 0) {
-                    HK[slot] = k;
-                    HM[slot] = meta;
-                    sp<uint32_t>(ly.h_used)[npiv] = slot;
-                }
-                return true;
+        int slot = ins_slot;
+        if (slot < 0) {  // the lookup saw no empty slot: probe
+            const uint32_t base = hmix(k) & hmask;
+            for (uint32_t probe = 0; probe <= hmask && slot < 0; probe += kWave) {
+                const uint64_t emp = ballot(HK[(base + probe + (uint32_t)lane) & hmask] == 0ull);
+                if (emp) slot = (int)((base + probe + (uint32_t)(__ffsll((unsigned long long)emp) - 1)) & hmask);
             }
+            if (slot < 0) return false;
+        }
+        if (lane == 0) {
+            HK[slot] = k;
+            HM[slot] = meta;
+            sp<uint32_t>(ly.h_used)[npiv] = (uint32_t)slot;
         }
         return true;
     }
 
-    // Owner of the pivot tau (see betti_wide.hip lookup): the pivot table's first 64-slot window
-    // and tau's edge lengths loaded together; a table hit returns its metadata, otherwise the
-    // apparent owner (tau's F-max facet f if tau is f's minimal cofacet) from the edge lengths in
-    // registers and one min-cofacet table read. kNoMeta if tau is not in the table.
-    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, uint32_t& app) const {
+    // Inserted vertex of the F-minimal cofacet of f (dim 1: edge, dim 2: triangle; packed) over
+    // the common neighbours of f's vertices, lane-parallel from the LDS matrix: the minimal
+    // (diameter, -vertex) — the walk's result in pass_dim1 / pass_dim2 (the first k walking
+    // downwards with the smallest diameter). kNone if f has no cofacet.
+    __device__ uint32_t min_cofacet_vertex(int dim, uint64_t f) const {
+        const int a = dim == 1 ? pv(f, 1) : pv(f, 2);
+        const int b = dim == 1 ? pv(f, 0) : pv(f, 1);
+        const int c = pv(f, 0);
+        const uint32_t ds = sdiam(dim, f);
+        uint32_t best = kNone;
+#pragma unroll
+        for (int t = 0; t < KW; ++t) {
+            if (t >= W) break;
+            uint64_t am = aw(a, t) & aw(b, t);
+            if (dim == 2) am &= aw(c, t);
+            const int x = min(64 * t + lane, n - 1);
+            const uint32_t dd = max(max(ds, dim == 2 ? d(c, x) : 0u), max(d(a, x), d(b, x)));
+            const uint32_t key = (dd << 16) | (uint32_t)(511 - (64 * t + lane));
+            if ((am >> lane) & 1ull) best = min(best, key);
+        }
+        const uint32_t m = wave_min32(best);
+        return m == kNone ? kNone : (uint32_t)(511 - (int)(m & 0xFFFFu));
+    }
+
+    // Owner of the pivot tau (wave 0): the pivot table's first 64-slot window (a hit returns its
+    // metadata), else the apparent owner — tau's F-max facet f, if tau is f's F-minimal cofacet —
+    // re-derived from the LDS matrix (app = f's packed vertices), else kNoMeta / kNone. A miss
+    // leaves the window's first empty slot in ins_slot for the insert.
+    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, uint32_t& app) {
         const uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint64_t* HM = sp<uint64_t>(ly.h_meta);
-        const uint32_t mask = (uint32_t)ly.h_cap - 1u;
-        const uint32_t slot = (hmix(tau) + (uint32_t)lane) & mask;
+        const uint32_t base = hmix(tau) & hmask;
+        const uint32_t slot = (base + (uint32_t)lane) & hmask;
         const uint64_t hk = HK[slot];
         const uint64_t hm = HM[slot];
         const int nv = dim + 2;
         const int v0 = pv(tv, nv - 1), v1 = pv(tv, nv - 2), v2 = pv(tv, nv - 3), v3 = nv == 4 ? pv(tv, 0) : 0;
-        const int np = nv == 4 ? 6 : 3;
-        const int lp = lane < np ? lane : 0;
-        const int ps = (int)(((nv == 4 ? 0x211000u : 0x100u) >> (4 * lp)) & 0xFu);
-        const int pt = (int)(((nv == 4 ? 0x332321u : 0x221u) >> (4 * lp)) & 0xFu);
-        const int va = ps == 0 ? v0 : (ps == 1 ? v1 : v2);
-        const int vb = pt == 1 ? v1 : (pt == 2 ? v2 : v3);
-        const uint32_t dl = d(va, vb);
-        const uint64_t hit = ballot(hk == tau), emp = ballot(hk == 0ull);
-        const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
-        const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
-        app = kNone;
-        if (fh < fe) return rl64(hm, fh);
-        if (fe == kWave) {
-            const uint64_t mm = hfind(tau);
-            if (mm != kNoMeta) return mm;
-        }
+        // F-max facet of tau from its edge lengths (the largest key: largest diameter, then the
+        // smallest index), computed while the table window is in flight
         uint32_t dd[4][4];
+        dd[0][1] = d(v0, v1);
+        dd[0][2] = d(v0, v2);
+        dd[1][2] = d(v1, v2);
         if (nv == 4) {
-            dd[0][1] = rl(dl, 0);
-            dd[0][2] = rl(dl, 1);
-            dd[0][3] = rl(dl, 2);
-            dd[1][2] = rl(dl, 3);
-            dd[1][3] = rl(dl, 4);
-            dd[2][3] = rl(dl, 5);
-        } else {
-            dd[0][1] = rl(dl, 0);
-            dd[0][2] = rl(dl, 1);
-            dd[1][2] = rl(dl, 2);
+            dd[0][3] = d(v0, v3);
+            dd[1][3] = d(v1, v3);
+            dd[2][3] = d(v2, v3);
         }
         const int v[4] = {v0, v1, v2, v3};
         uint64_t bestk = 0, bestf = 0;
         int drop = 0;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < 4; ++t) {  // facet without v[t]
             if (t >= nv) break;
             uint32_t diam = 0;
             uint64_t f = 0;
@@ -643,9 +710,19 @@ struct WgCx {
                 drop = t;
             }
         }
-        const uint16_t mcv = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
+        const uint64_t hit = ballot(hk == tau), emp = ballot(hk == 0ull);
+        const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
+        const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
+        app = kNone;
+        if (fh < fe) return rl64(hm, fh);
+        if (fe < kWave) {
+            ins_slot = (int)((base + (uint32_t)fe) & hmask);
+        } else {  // the window was full: probe on (rare at load factor <= 1/2)
+            const uint64_t mm = hfind(tau);
+            if (mm != kNoMeta) return mm;
+        }
         const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
-        if (uni(mcv) == (uint32_t)vd) app = (uint32_t)bestf;
+        if (min_cofacet_vertex(dim, bestf) == (uint32_t)vd) app = (uint32_t)bestf;
         return kNoMeta;
     }
 
@@ -682,143 +759,130 @@ struct WgCx {
         return true;
     }
 
-    // Pivot of sum(delta s, s in V) above `floor`: the (V entry, bitset word) pairs are dealt to
-    // the waves; lane k of a pair (s, t) evaluates the cofacet s u {64 t + k}; each wave's minimum
-    // and its multiplicity go through LDS; the combined minimum with odd multiplicity is the pivot,
-    // even: raise the floor and repeat. kInf for the zero column.
-    __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
+    // One wave's share of a pivot search (every wave): the (V entry, bitset word) pairs p = e W + t,
+    // p = wv, wv + kNW, ...; lane k of a pair (s, t) evaluates the cofacet s u {64 t + k} (32-bit
+    // combinatorial index: the partial sums of s's vertices plus x's binomial at its position; the
+    // packed cofacet is built once, for the winning lane). Writes the wave's minimum above
+    // `floor`, its multiplicity and the packed cofacet to the wave's LDS slot.
+    __device__ void search_share(int dim, int v, uint64_t floor) {
         const int k = lane;
-        WG_COUNT(29, 1);  // pivot searches
+        uint64_t lmin = kInf;
+        int lcnt = 0, lx = 0;
+        uint32_t ls = 0;
+        auto eval = [&](uint32_t s, uint32_t ds, int t) __attribute__((always_inline)) {
+            const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
+            const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
+            const int c = pv(s, 0);
+            const int x = 64 * t + k;
+            const int xr = min(x, n - 1);
+            const uint32_t da = d(a, xr), db = d(b, xr), dc = dim == 2 ? d(c, xr) : 0u;
+            uint64_t am = aw(a, t) & aw(b, t);
+            if (dim == 2) am &= aw(c, t);
+            const uint32_t dd = max(max(ds, dc), max(da, db));
+            const uint32_t ux = (uint32_t)x;
+            const uint32_t ua = (uint32_t)a, ubb = (uint32_t)b, uc = (uint32_t)c;
+            uint32_t idx;
+            if (dim == 1) {  // triangle (a, b) u {x}
+                idx = x > a ? b3(ux) + b2(ua) + ubb : (x > b ? b3(ua) + b2(ux) + ubb : b3(ua) + b2(ubb) + ux);
+            } else {  // tetrahedron (a, b, c) u {x}
+                const uint32_t a4 = b4(ua), a3 = b3(ua), bb3 = b3(ubb), bb2 = b2(ubb);
+                idx = x > a ? b4(ux) + a3 + bb2 + uc
+                            : (x > b ? a4 + b3(ux) + bb2 + uc
+                                     : (x > c ? a4 + bb3 + b2(ux) + uc : a4 + bb3 + b2(uc) + ux));
+            }
+            const uint64_t kk = wkey(dd, idx);
+            if (((am >> k) & 1ull) && kk > floor) {
+                if (kk < lmin) {
+                    lmin = kk;
+                    lcnt = 1;
+                    ls = s;
+                    lx = x;
+                } else if (kk == lmin) {
+                    ++lcnt;
+                }
+            }
+        };
+        int e = 0, t = wv;
+        while (t >= W) {
+            t -= W;
+            ++e;
+        }
+        while (e < v) {
+            const uint32_t s = wg_ctl.vl[e], ds = wg_ctl.vd[e];
+            int e2 = e, t2 = t + kNW;
+            while (t2 >= W) {
+                t2 -= W;
+                ++e2;
+            }
+            if (e2 < v) {  // two pairs' reads in flight together
+                const uint32_t s2 = wg_ctl.vl[e2], ds2 = wg_ctl.vd[e2];
+                eval(s, ds, t);
+                eval(s2, ds2, t2);
+                e = e2;
+                t = t2 + kNW;
+                while (t >= W) {
+                    t -= W;
+                    ++e;
+                }
+            } else {
+                eval(s, ds, t);
+                e = e2;
+                t = t2;
+            }
+        }
+        const uint64_t m = wave_min(lmin);
+        const int cnt = wave_sum(lmin == m ? lcnt : 0);
+        uint64_t pk = 0;
+        if (m != kInf) {
+            const int wl = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
+            pk = pinsert(dim + 1, rl(ls, wl), (int)rl((uint32_t)lx, wl));
+        }
+        wg_ctl.smin[wv] = m;  // every lane stores the same (uniform) values
+        wg_ctl.scnt[wv] = (uint32_t)cnt;
+        wg_ctl.spk[wv] = pk;
+    }
+
+    // helper waves (1..kNW-1) during a reduction: wake at barrier A for a search request posted by
+    // wave 0, evaluate their share, post it before barrier B; leave on the stop request
+    __device__ void helper_loop() {
         for (;;) {
-            uint64_t lmin = kInf, lp = 0;
-            int lcnt = 0;
-#ifdef DGN_WG_FASTKEY
-            // 32-bit combinatorial index of s u {x} (C(362, 4) < 2^32): the uniform partial sums of
-            // s's vertices plus x's binomial at its position; the packed cofacet is built once,
-            // for the winning lane (its entry s and vertex x are tracked instead)
-            uint32_t ls = 0;
-            int lx = 0;
-            auto eval = [&](uint32_t s, uint32_t ds, int t) __attribute__((always_inline)) {
-                const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
-                const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
-                const int c = pv(s, 0);
-                const int x = 64 * t + k;
-                const int xr = min(x, n - 1);
-                const uint32_t da = d(a, xr), db = d(b, xr), dc = dim == 2 ? d(c, xr) : 0u;
-                uint64_t am = aw(a, t) & aw(b, t);
-                if (dim == 2) am &= aw(c, t);
-                const uint32_t dd = max(max(ds, dc), max(da, db));
-                const uint32_t ux = (uint32_t)x;
-                const uint32_t x2 = ux * (ux - 1u) / 2u, x3 = x2 * (ux - 2u) / 3u, x4 = x3 * (ux - 3u) / 4u;
-                const uint32_t ua = (uint32_t)a, ub_ = (uint32_t)b, uc = (uint32_t)c;
-                const uint32_t a2 = ua * (ua - 1u) / 2u, a3 = a2 * (ua - 2u) / 3u;
-                const uint32_t b2 = ub_ * (ub_ - 1u) / 2u;
-                uint32_t idx;
-                if (dim == 1) {  // triangle (a, b) u {x}
-                    idx = x > a ? x3 + a2 + ub_ : (x > b ? a3 + x2 + ub_ : a3 + b2 + ux);
-                } else {  // tetrahedron (a, b, c) u {x}
-                    const uint32_t a4 = a3 * (ua - 3u) / 4u, b3 = b2 * (ub_ - 2u) / 3u;
-                    const uint32_t c2 = uc * (uc - 1u) / 2u;
-                    idx = x > a ? x4 + a3 + b2 + uc
-                                : (x > b ? a4 + x3 + b2 + uc : (x > c ? a4 + b3 + x2 + uc : a4 + b3 + c2 + ux));
-                }
-                const uint64_t kk = ((uint64_t)dd << 32) | (uint64_t)(~idx);
-                if (((am >> k) & 1ull) && kk > floor) {
-                    if (kk < lmin) {
-                        lmin = kk;
-                        lcnt = 1;
-                        ls = s;
-                        lx = x;
-                    } else if (kk == lmin) {
-                        ++lcnt;
-                    }
-                }
-            };
-#else
-            auto eval = [&](uint32_t s, uint32_t ds, int t) __attribute__((always_inline)) {
-                const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
-                const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
-                const int c = pv(s, 0);
-                const int x = 64 * t + k;
-                const int xr = min(x, n - 1);
-                const uint32_t da = d(a, xr), db = d(b, xr), dc = dim == 2 ? d(c, xr) : 0u;
-                uint64_t am = aw(a, t) & aw(b, t);
-                if (dim == 2) am &= aw(c, t);
-                const uint32_t dd = max(max(ds, dc), max(da, db));
-                const uint64_t p = pinsert(dim + 1, s, x);
-                const uint64_t kk = wkey(dd, pidx(dim + 2, p));
-                if (((am >> k) & 1ull) && kk > floor) {
-                    if (kk < lmin) {
-                        lmin = kk;
-                        lcnt = 1;
-                        lp = p;
-                    } else if (kk == lmin) {
-                        ++lcnt;
-                    }
-                }
-            };
-#endif
-            // pairs p = e W + t, p = wv, wv + kNW, ...: (e, t) stepped without division
-            int e = 0, t = wv;
-            while (t >= W) {
-                t -= W;
-                ++e;
+            sync_lds();  // A
+            if (uni((uint32_t)wg_ctl.rq_stop)) break;
+            const int dim = (int)uni((uint32_t)wg_ctl.rq_dim), v = (int)uni((uint32_t)wg_ctl.rq_v);
+            const uint64_t floor = uni64(wg_ctl.rq_floor);
+            search_share(dim, v, floor);
+            sync_lds();  // B
+        }
+    }
+
+    // Pivot of sum(delta s, s in V) above `floor` (wave 0 with the helpers): the combined minimum
+    // with odd multiplicity; even: raise the floor and repeat. kInf for the zero column.
+    __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
+        WG_COUNT(29, 1);
+        for (;;) {
+            if (lane == 0) {
+                wg_ctl.rq_floor = floor;
+                wg_ctl.rq_v = v;
+                wg_ctl.rq_dim = dim;
+                wg_ctl.rq_stop = 0;
             }
-            while (e < v) {
-                const uint32_t s = wg_ctl.vl[e], ds = wg_ctl.vd[e];
-                int e2 = e, t2 = t + kNW;
-                while (t2 >= W) {
-                    t2 -= W;
-                    ++e2;
-                }
-                if (e2 < v) {  // two pairs' reads in flight together
-                    const uint32_t s2 = wg_ctl.vl[e2], ds2 = wg_ctl.vd[e2];
-                    eval(s, ds, t);
-                    eval(s2, ds2, t2);
-                    e = e2;
-                    t = t2 + kNW;
-                    while (t >= W) {
-                        t -= W;
-                        ++e;
-                    }
-                } else {
-                    eval(s, ds, t);
-                    e = e2;
-                    t = t2;
-                }
-            }
-            const uint64_t m = wave_min(lmin);
-            const int cnt = wave_sum(lmin == m ? lcnt : 0);
-            uint64_t pk = 0;
-#ifdef DGN_WG_FASTKEY
-            if (m != kInf) {
-                const int wl = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
-                pk = pinsert(dim + 1, rl(ls, wl), (int)rl((uint32_t)lx, wl));
-            }
-            (void)lp;
-#else
-            if (m != kInf) pk = rl64(lp, __ffsll((unsigned long long)ballot(lmin == m)) - 1);
-#endif
-            const int r = rnd & 1;
-            wg_ctl.smin[r][wv] = m;  // every lane stores the same (uniform) values
-            wg_ctl.scnt[r][wv] = (uint32_t)cnt;
-            wg_ctl.spk[r][wv] = pk;
-            __syncthreads();
-            ++rnd;
+            sync_lds();  // A
+            search_share(dim, v, floor);
+            sync_lds();  // B
             uint64_t M = kInf, PK = 0;
             uint32_t C = 0;
 #pragma unroll
             for (int q = 0; q < kNW; ++q) {
-                const uint64_t mq = wg_ctl.smin[r][q];
+                const uint64_t mq = wg_ctl.smin[q];
                 if (mq < M) {
                     M = mq;
                     C = 0;
-                    PK = wg_ctl.spk[r][q];
+                    PK = wg_ctl.spk[q];
                 }
-                if (mq == M) C += wg_ctl.scnt[r][q];
+                if (mq == M) C += wg_ctl.scnt[q];
             }
             M = uni64(M);
-            WG_COUNT(30, 1);  // floor rounds
+            WG_COUNT(30, 1);
             if (M == kInf) return kInf;
             if (uni(C) & 1u) {
                 tv = uni64(PK);
@@ -828,15 +892,40 @@ struct WgCx {
         }
     }
 
-    // ---- the non-apparent columns of one dimension, in Ripser's order (every wave) ----
-    __device__ void reduce(int dim, int nna) {
-        if (nna > ly.na_cap) {
+    // ---- the non-apparent columns of one dimension, in Ripser's order ----
+    __device__ void reduce(int dim, int cnt) {
+        if (cnt > ly.na_cap) {  // uniform: the column counter is shared
             err |= kENA;
             return;
         }
         WG_MARK(-1);
-        sort_na(nna);
+        const int nna = sort_na(dim, cnt);
         WG_MARK(16);
+        // pivot table slots for this reduction: >= 2 nna (load factor <= 1/2), >= one window
+        uint32_t hc = 64;
+        while (hc < 2u * (uint32_t)nna && hc < (uint32_t)ly.h_cap) hc <<= 1;
+        hmask = hc - 1u;
+        if (wv != 0) {
+            helper_loop();
+        } else {
+            reduce_driver(dim, nna);
+            if (lane == 0) {
+                wg_ctl.rq_stop = 1;
+                wg_ctl.err = err;
+            }
+            sync_lds();  // A: the helpers leave
+        }
+        __syncthreads();
+        err = uni(wg_ctl.err);
+        // empty the pivot table for the next dimension / complex
+        uint64_t* HK = sp<uint64_t>(ly.h_key);
+        const uint32_t* used = sp<uint32_t>(ly.h_used);
+        const int npiv = (int)uni((uint32_t)wg_ctl.npiv);
+        for (int i = threadIdx.x; i < npiv; i += kWgThreads) HK[used[i]] = 0ull;
+        __syncthreads();
+    }
+
+    __device__ void reduce_driver(int dim, int nna) {
         const uint64_t* K = sp<uint64_t>(ly.na_key);
         const uint32_t* P = sp<uint32_t>(ly.na_perm);
         const uint64_t* T = sp<uint64_t>(ly.na_tau);
@@ -873,38 +962,23 @@ struct WgCx {
             int v = 0;  // 0 = lazy: V == {this column}
             if (meta != kNoMeta || app != kNone) {
                 WG_COUNT(22, 1);  // columns that need a reduction
-                bool first = true;
+                bool ok = v_toggle(dim, cp, v);
                 int64_t guard = 0;
                 for (;;) {
-                    const int r = rnd & 1;
-                    if (wv == 0) {
-                        bool ok = true;
-                        int vv = v;
-                        if (first) {
-                            vv = 0;
-                            ok = v_toggle(dim, cp, vv);
+                    if (app != kNone) {
+                        ok = ok && v_toggle(dim, app, v);
+                    } else if (meta & kLazy) {
+                        ok = ok && v_toggle(dim, (uint32_t)(meta & ~kLazy), v);
+                    } else {
+                        const int64_t off = (int64_t)(meta >> kMetaLenBits);
+                        const int len = (int)(meta & ((1ull << kMetaLenBits) - 1));
+                        for (int t0 = 0; t0 < len && ok; t0 += kWave) {
+                            const uint32_t w = t0 + lane < len ? vstore[off + t0 + lane] : 0u;
+                            const int c = len - t0 < kWave ? len - t0 : kWave;
+                            for (int u = 0; u < c && ok; ++u) ok = v_toggle(dim, rl(w, u), v);
                         }
-                        if (app != kNone) {
-                            ok = ok && v_toggle(dim, app, vv);
-                        } else if (meta & kLazy) {
-                            ok = ok && v_toggle(dim, (uint32_t)(meta & ~kLazy), vv);
-                        } else {
-                            const int64_t off = (int64_t)(meta >> kMetaLenBits);
-                            const int len = (int)(meta & ((1ull << kMetaLenBits) - 1));
-                            for (int t0 = 0; t0 < len && ok; t0 += kWave) {
-                                const uint32_t w = t0 + lane < len ? vstore[off + t0 + lane] : 0u;
-                                const int cnt = len - t0 < kWave ? len - t0 : kWave;
-                                for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(dim, rl(w, u), vv);
-                            }
-                        }
-                        wg_ctl.vv[r] = vv;
-                        wg_ctl.vok[r] = ok ? 1u : 0u;
                     }
-                    __syncthreads();
-                    ++rnd;
-                    first = false;
-                    v = (int)uni((uint32_t)wg_ctl.vv[r]);
-                    if (!uni(wg_ctl.vok[r])) {
+                    if (!ok) {
                         err |= kEWork;
                         break;
                     }
@@ -926,10 +1000,10 @@ struct WgCx {
             }
             const uint32_t death = kdiam(tau), birth = kdiam(colkey);
             if (death > birth) {  // codes preserve order: value(death) > value(birth)
-                if (wv == 0 && lane == 0 && np < ly.p_cap) pairs[np] = make_uint2(birth, death);
+                if (lane == 0 && np < ly.p_cap) pairs[np] = make_uint2(birth, death);
                 ++np;
             }
-            if (dim == 1 && wv == 0 && lane == 0) sp<uint16_t>(ly.mc_t)[pidx(3, tv)] = kMcCleared;  // clearing
+            if (dim == 1) clear_mark(lane == 0, pidx(3, tv));  // clearing for dim 2
             uint64_t mt;
             if (v == 0) {
                 mt = kLazy | cp;
@@ -938,28 +1012,17 @@ struct WgCx {
                     err |= kER;
                     break;
                 }
-                if (wv == 0)
-                    for (int t = lane; t < v; t += kWave) vstore[vused + t] = wg_ctl.vl[t];
+                for (int t = lane; t < v; t += kWave) vstore[vused + t] = wg_ctl.vl[t];
                 mt = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;
             }
-            WG_MARK(-1);
-            // every wave's last lookup of this column reads the table before wave 0 inserts tau (a
-            // lagging wave that saw tau's own entry would take another reduction round alone)
-            __syncthreads();
             if (!hinsert(tau, mt, npiv)) {
                 err |= kEPiv;
                 break;
             }
             ++npiv;
-            __syncthreads();  // wave 0's table insert, V store and clearing mark before the next column
         }
-        __syncthreads();
-        // empty the pivot table for the next dimension / complex
-        uint64_t* HK = sp<uint64_t>(ly.h_key);
-        const uint32_t* used = sp<uint32_t>(ly.h_used);
-        for (int i = threadIdx.x; i < npiv; i += kWgThreads) HK[used[i]] = 0ull;
-        __syncthreads();
+        if (lane == 0) wg_ctl.npiv = npiv;
     }
 
     // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) + outputs (wave 0) ----
@@ -1004,42 +1067,40 @@ struct WgCx {
         }
     }
 
+    // reset the clearing bits this complex set (their words are listed): every complex starts with
+    // an all-zero bitset
+    __device__ void clear_reset() {
+        __syncthreads();
+        const int nl = (int)uni(wg_ctl.ctr[4]);
+        uint32_t* clr = sp<uint32_t>(ly.mc_t);
+        const uint32_t* lst = sp<uint32_t>(ly.mc_e);
+        for (int i = threadIdx.x; i < nl; i += kWgThreads) clr[lst[i]] = 0u;
+    }
+
     __device__ void run(int64_t gi, int64_t slot, double weight) {
         WG_MARK(-1);
         load(slot);
         WG_MARK(0);
-        if (threadIdx.x < 4) wg_ctl.ctr[threadIdx.x] = 0u;
-        if (wv == 0) {
-            prim();
-        } else if (wv == 1) {
-            const int ne = edge_list();
-            wg_ctl.nedges = ne;  // every lane stores the same value
-        }
+        if (threadIdx.x < 6) wg_ctl.ctr[threadIdx.x] = 0u;
+        if (wv == 0) prim();
         __syncthreads();
-        const int n_edges = (int)uni((uint32_t)wg_ctl.nedges);
         WG_MARK(1);
-        WG_COUNT(10, n_edges);
-        pass_dim1(n_edges);
+        pass_dim1();
         __syncthreads();
         WG_MARK(2);
         WG_COUNT(8, uni(wg_ctl.ctr[2]));
         reduce(1, (int)uni(wg_ctl.ctr[2]));
         WG_MARK(3);
-        // reduce ends with a barrier: the clearing marks are complete before the dim-2 pass
+        // the reduction ends with a barrier: the clearing marks are complete before the filter
         if (err == 0u) {
-            pass_dim2(n_edges);
+            pass_dim2();
             __syncthreads();
             WG_MARK(4);
             WG_COUNT(9, uni(wg_ctl.ctr[3]));
             reduce(2, (int)uni(wg_ctl.ctr[3]));
             WG_MARK(5);
-        } else {
-            // no dim-2 pass consumes the clearing marks: erase every triangle entry
-            uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
-            const int64_t nt = (int64_t)bin3((uint64_t)n);
-            for (int64_t t = threadIdx.x; t < nt; t += kWgThreads) mc_t[t] = kMcNone;
-            __syncthreads();
         }
+        clear_reset();
         if (wv == 0) finish(gi, weight);
         __syncthreads();
         WG_MARK(6);
@@ -1057,7 +1118,6 @@ __global__ __launch_bounds__(kWgThreads) void betti_wg_kernel(BettiLaunch bl, Wi
     const int lane = lane_id();
     uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
     const int64_t total = (int64_t)*bl.wide_len;
-    uint32_t rnd = 0;
     for (int it = 0;; ++it) {
         // dequeue: wave 0's lanes all execute the atomic (lane 0 adds 1), the ticket goes through LDS
         if (wv == 0) {
@@ -1077,10 +1137,9 @@ __global__ __launch_bounds__(kWgThreads) void betti_wg_kernel(BettiLaunch bl, Wi
             }
             continue;
         }
-        WgCx<KW> cx{bl, ly, adj, par, Dm, scr, n, (n + 63) / 64, wv, lane, 0u, false, 0u, 0, 0, 0, 0, rnd,
-                    bl.rank_sorted + wi * bl.rank_stride};
+        WgCx<KW> cx{bl, ly, adj, par, Dm, scr, n, (n + 63) / 64, wv, lane, 0u, false, 0u, 0, 0, 0, 0,
+                    bl.rank_sorted + wi * bl.rank_stride, 63u, -1};
         cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
-        rnd = cx.rnd;
         if (bl.retried && wv == 0 && lane == 0) atomicAdd(bl.retried, 1u);
     }
 }
@@ -1114,7 +1173,7 @@ int betti_wg_resident_blocks(int device, int nmax) {
 
 hipError_t launch_betti_wg(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int blocks) {
     if (blocks <= 0) return hipSuccess;
-    if (!b.rank_codes || !b.rank_sorted || !betti_wg_supported(l.nmax)) return hipErrorInvalidValue;
+    if (!b.rank_codes || !b.rank_sorted || !betti_wg_supported(l.nmax) || !l.wg) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wg_kernel_for(l.nmax), dim3((unsigned)blocks), dim3(kWgThreads), betti_wg_lds_bytes(l.nmax), st,
                        b, l);
     return hipGetLastError();

@@ -1189,8 +1189,9 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix)
         return at;
     };
     l.D = take(matrix ? 4 * n * n : 0);
-    l.mc_e = take(2 * e);
-    l.mc_t = take(2 * t);
+    l.wg = matrix ? 0 : 1;
+    l.mc_e = take(matrix ? 2 * e : 4 * e);
+    l.mc_t = take(matrix ? 2 * t : (t + 31) / 32 * 4);
     l.edges = take(4 * e);
     l.na_key = take(8 * cap);
     l.na_tau = take(8 * cap);
@@ -1213,7 +1214,9 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix)
 hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves) {
     hipError_t e = hipMemset2DAsync(l.base + l.h_key, (size_t)l.total, 0, 8 * (size_t)l.h_cap, (size_t)waves, s);
     if (e != hipSuccess) return e;
-    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges
+    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges; the workgroup
+    // layout's clearing bitset (mc_t .. edges) starts all zero
+    if (l.wg) return hipMemset2DAsync(l.base + l.mc_t, (size_t)l.total, 0, (size_t)(l.edges - l.mc_t), (size_t)waves, s);
     return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
 }
 

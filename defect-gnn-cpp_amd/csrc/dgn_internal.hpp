@@ -145,6 +145,8 @@ struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
     int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
+    int32_t wg;     // workgroup-kernel layout (matrix = false): mc_e = cleared-triangle list (u32 per
+                    // edge), mc_t = clearing bitset (a bit per triangle, starts and ends all zero)
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
     int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, na_perm, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2,
         d0;

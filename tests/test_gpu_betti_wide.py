@@ -16,6 +16,9 @@ def _ref(low, n, thr):
     return O.ref_persistence(low, n, thr) if O.ref_available() else O.persistence(low, n, thr)
 
 
+WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG
+
+
 def _check_clouds(ctx, clouds, npts, thr, cap):
     pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=cap)
     bad = []
@@ -56,11 +59,21 @@ def test_all_three_tiers_in_one_batch(ctx):
 
 
 @pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
-def test_fcc256_default_cutoff_10A(ctx):
+@pytest.mark.parametrize("wg", [0, 1])
+def test_fcc256_default_cutoff_10A(ctx, wg):
     """compute_structure_betti_features at the reference default r_cutoff = 10 (~340-point
-    complexes); spot-check atoms against the verbatim Ripser."""
+    complexes), with the one-wave and the workgroup-per-complex wide kernels; spot-check atoms
+    against the verbatim Ripser, and the two kernels against each other on every atom."""
     batch = dgn.synth_batch("fcc", 4, 1)
-    f, c = ctx.host_betti(batch, 10.0)
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, wg)
+    try:
+        f, c = ctx.host_betti(batch, 10.0)
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 1 - wg)
+        f2, c2 = ctx.host_betti(batch, 10.0)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, WG_DEFAULT)
+    assert np.array_equal(c, c2)
+    np.testing.assert_allclose(f, f2, rtol=FEAT_RTOL, atol=FEAT_ATOL)
     assert not np.isnan(f).any()
     atoms = [0, 77, 200]
     fo, co = O.ref_atom_betti(batch["lattice"][0], batch["positions"], batch["species"], 10.0, atoms)
@@ -100,9 +113,6 @@ def test_f32_fallback_matches_rank_codes(ctx):
         for d, col in ((0, 0), (1, 2), (2, 3)):
             n = k16[c, col]
             assert np.array_equal(p32[c, d, :n], p16[c, d, :n]), (c, d)
-
-
-WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG
 
 
 def test_workgroup_kernel_matches_wave_kernel(ctx):
