@@ -341,8 +341,32 @@ struct Complex {
     // cleared triangles hold kNone), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         const uint32_t f = uni(max_facet(dim, uni64(tau)));
+#ifdef DGN_APP_LDS
+        // f's F-minimal cofacet re-derived from the LDS matrix instead of the scratch table (one
+        // dependent global read less per owner lookup): lane k = candidate vertex k; the minimal
+        // diameter, then the largest k (the lane pass's walk). Tree edges and cleared triangles
+        // need no mark: such an f is already in a persistence pair (dim 0 / dim 1), so it is
+        // never in an apparent pair and the test below fails for it by itself.
+        const int k = lane_id();
+        const int a = dim == 1 ? (int)((f >> 8) & 255) : (int)((f >> 16) & 255);
+        const int b = dim == 1 ? (int)(f & 255) : (int)((f >> 8) & 255);
+        const int c = (int)(f & 255);
+        const uint32_t ds = dim == 1 ? dlowb(a, b) : tri_diamb(a, b, c);
+        uint32_t dd = max(Db()[a * S + k], Db()[b * S + k]);
+        if (dim == 2) dd = max(dd, Db()[c * S + k]);
+        // k is a common neighbour iff every distance is <= thr (the +inf diagonal excludes f's own
+        // vertices; lanes k >= n read past the rows and are not vertices)
+        const bool ok = k < n && dd <= __float_as_uint(thr);
+        const uint32_t key = ok ? max(dd, ds) : 0xFFFFFFFFu;
+        const uint32_t m = wave_min_u32(key);
+        const uint64_t bal = ballot(ok && key == m);
+        if (!bal) return kNone;
+        const uint32_t kb = (uint32_t)(63 - __clzll((long long)bal));
+        return kb == extra_vertex(key_packed(tau), f) ? f : kNone;
+#else
         const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
         return uni(m) == extra_vertex(key_packed(tau), f) ? f : kNone;
+#endif
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {

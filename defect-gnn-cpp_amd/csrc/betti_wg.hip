@@ -9,10 +9,10 @@
 // complex's u16 rank codes (betti_rank_codes: order- and equality-preserving, C(362, 2) < 2^16)
 // sit in LDS as the packed lower triangle (<= 128 KB) next to the adjacency bitsets (<= 17 KB),
 // so every distance read is an LDS read, and no per-simplex table lives in memory at all:
-//   * load, adjacency: all waves;  Prim: wave 0;
-//   * dim-1 / dim-2 apparent passes: lane per column, the edges dealt to the lanes as (row, bitset
-//     word) units of the LDS adjacency from an LDS counter — no edge list in memory (dim 2: a
-//     per-lane work queue over the edges' triangles, as betti_wide.hip). No min-cofacet
+//   * load, adjacency: all waves;  Prim (wave 0) beside the edge list (wave 1);
+//   * dim-1 / dim-2 apparent passes: lane per column, the edges dealt to the lanes from an LDS
+//     counter, each lane's next edge prefetched (dim 2: a per-lane work queue over the edges'
+//     triangles, as betti_wide.hip). No min-cofacet
 //     tables: the reduction re-derives an apparent owner from the LDS matrix when it needs one
 //     (lane-parallel, a few hundred cycles instead of a scattered HBM read);
 //   * clearing: the dim-1 pivots (apparent and reduced) set a bit per triangle in a scratch bitset;
@@ -41,6 +41,7 @@ namespace {
 #define WG_LDS __attribute__((address_space(3)))
 
 constexpr int kNW = DGN_WG_WAVES;          // waves per workgroup (per complex)
+static_assert(kNW >= 2, "Prim and the edge list run on two waves");
 constexpr int kWgThreads = kNW * kWave;
 constexpr int kVlCap = 512;                // V list entries (LDS); more: capacity retry
 constexpr uint64_t kInf = ~0ull;
@@ -58,7 +59,8 @@ constexpr uint64_t VM = (1ull << VB) - 1;
 // control block (static LDS)
 struct WgCtl {
     uint32_t ticket[2];  // complex dequeue (double-buffered by iteration parity)
-    uint32_t ctr[6];     // dim-1 / dim-2 edge units, dim-1 / dim-2 columns, clear list
+    uint32_t ctr[6];     // dim-1 edge chunks, dim-2 edges, dim-1 / dim-2 columns, clear list
+    int32_t nedges;
     uint32_t err;        // wave 0's error bits after a reduction
     // pivot-search request (wave 0 -> helper waves) and the per-wave results
     uint64_t rq_floor;
@@ -273,46 +275,19 @@ struct WgCx {
         }
     }
 
-    // ---- edge source of the lane-parallel passes: units (row i, bitset word w), u = i W + w,
-    // dealt from an LDS counter; a unit holds the edges (i, j), j < i, of word w (read from the LDS
-    // adjacency: no edge list in memory). Lanes with no edge left take new units together. ----
-    struct EdgeSrc {
-        int ui = 0;         // current unit's row
-        int uw = 0;         // current unit's word
-        uint64_t ub = 0;    // its remaining j bits
-        bool drained = false;
-    };
-    // every lane without edges left gets a unit with at least one edge, or the counter is drained
-    __device__ void units_refill(EdgeSrc& es, uint32_t* ctr, bool want) const {
-        for (;;) {
-            const bool need = want && es.ub == 0ull && !es.drained;
-            const uint64_t bal = ballot(need);
-            if (!bal) return;
-            const uint32_t base = lds_add_uniform(ctr, (uint32_t)__popcll(bal));
-            if (need) {
-                const int u = (int)(base + (uint32_t)mask_prefix(bal));
-                if (u >= n * W) {
-                    es.drained = true;
-                } else {
-                    const int i = u / W, w = u - i * W;
-                    uint64_t bits = 64 * w < i ? aw(i, w) : 0ull;
-                    const int lim = i - 64 * w;
-                    if (lim < 64) bits &= (1ull << (lim > 0 ? lim : 0)) - 1ull;
-                    es.ui = i;
-                    es.uw = w;
-                    es.ub = bits;
-                }
+    // ---- edges (i > j, d <= thr) in index order (wave 1, beside Prim) ----
+    __device__ int edge_list() {
+        uint32_t* edges = sp<uint32_t>(ly.edges);
+        int off = 0;
+        for (int i = 1; i < n; ++i)
+            for (int w = 0; 64 * w < i; ++w) {
+                uint64_t bits = aw(i, w);
+                const int lim = i - 64 * w;
+                if (lim < 64) bits &= (1ull << lim) - 1ull;
+                if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = ((uint32_t)i << VB) | (uint32_t)(64 * w + lane);
+                off += __popcll(bits);
             }
-        }
-    }
-    // the lane's next edge (i > j) from its unit; false when the lane has none
-    __device__ bool units_next(EdgeSrc& es, int& i, int& j) const {
-        if (es.ub == 0ull) return false;
-        const int bit = __ffsll((unsigned long long)es.ub) - 1;
-        es.ub &= es.ub - 1ull;
-        i = es.ui;
-        j = 64 * es.uw + bit;
-        return true;
+        return off;
     }
 
     // append the lanes' non-apparent columns (lanes with `na`) through the LDS column counter
@@ -342,21 +317,24 @@ struct WgCx {
         }
     }
 
-    // ---- dim 1: lane per column (non-tree edge), edges from the LDS units ----
-    __device__ void pass_dim1() {
-        EdgeSrc es;
-        for (;;) {
-            units_refill(es, &wg_ctl.ctr[0], true);
-            int i = 0, j = 0;
-            const bool have = units_next(es, i, j);
-            if (!ballot(have)) break;
+    // ---- dim 1: lane per column (non-tree edge), 64-edge chunks dealt from an LDS counter; the
+    // next chunk's edge words are loaded while this one is walked ----
+    __device__ void pass_dim1(int n_edges) {
+        const uint32_t* edges = sp<uint32_t>(ly.edges);
+        int base = (int)lds_add_uniform(&wg_ctl.ctr[0], kWave);
+        uint32_t ed = base + lane < n_edges ? edges[base + lane] : 0u;
+        while (base < n_edges) {
+            const int e = base + lane;
+            const uint32_t cur = ed;
+            base = (int)lds_add_uniform(&wg_ctl.ctr[0], kWave);
+            ed = base + lane < n_edges ? edges[base + lane] : 0u;
             bool na = false, app = false;
             uint64_t colkey = 0, best = kInf, bestp = 0;
             uint32_t colp = 0;
-            if (have && !is_tree(i, j)) {
-                const uint32_t ed = ((uint32_t)i << VB) | (uint32_t)j;
+            const int i = (int)(cur >> VB), j = (int)(cur & VM);
+            if (e < n_edges && !is_tree(i, j)) {
                 const uint32_t dij = d(i, j);
-                colp = ed;
+                colp = cur;
                 colkey = wkey(dij, b2(i) + j);
                 // F-minimal cofacet: walking k downwards over the common neighbours, the first k
                 // with both distances <= d(i, j) ends the walk; before it, a smaller k wins only
@@ -385,7 +363,7 @@ struct WgCx {
                     }
                 }
                 if (bk >= 0) {
-                    bestp = pinsert(2, ed, bk);
+                    bestp = pinsert(2, cur, bk);
                     best = wkey(bd, pidx(3, bestp));
                     // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet
                     app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
@@ -401,8 +379,14 @@ struct WgCx {
     // from an LDS counter (see betti_wide.hip pass_dim2). Cleared triangles are walked too (they are
     // never apparent) and dropped from the column list by the sort's filter ----
     static constexpr int kStep = 4;
-    __device__ void pass_dim2() {
-        EdgeSrc es;
+    __device__ void pass_dim2(int n_edges) {
+        const uint32_t* edges = sp<uint32_t>(ly.edges);
+        // each lane's next edge word is prefetched when it takes an edge (kNone: none left)
+        uint32_t nxt;
+        {
+            const int e0 = (int)lds_add_uniform(&wg_ctl.ctr[1], kWave) + lane;
+            nxt = e0 < n_edges ? edges[e0] : kNone;
+        }
         int ea = 0, eb = 0, tw = -1;
         uint64_t tm = 0;
         bool act = false, fresh = false;
@@ -424,16 +408,18 @@ struct WgCx {
                     const int lim = eb - 64 * tw;
                     if (lim < 64) tm &= (1ull << lim) - 1ull;
                 }
-                const bool need = !act && tm == 0ull;
-                if (!ballot(need && (es.ub != 0ull || !es.drained))) break;
-                units_refill(es, &wg_ctl.ctr[1], need);
-                int i = 0, j = 0;
-                if (need && units_next(es, i, j)) {
-                    ea = i;
-                    eb = j;
+                const bool need = !act && tm == 0ull && nxt != kNone;
+                const uint64_t bal = ballot(need);
+                if (!bal) break;
+                const int base = (int)lds_add_uniform(&wg_ctl.ctr[1], (uint32_t)__popcll(bal));
+                if (need) {
+                    ea = (int)(nxt >> VB);
+                    eb = (int)(nxt & VM);
                     tw = 0;
                     tm = aw(ea, 0) & aw(eb, 0);
                     if (eb < 64) tm &= (1ull << eb) - 1ull;
+                    const int e = base + mask_prefix(bal);
+                    nxt = e < n_edges ? edges[e] : kNone;
                 }
             }
             if (!act && tm != 0ull) {
@@ -1082,10 +1068,17 @@ struct WgCx {
         load(slot);
         WG_MARK(0);
         if (threadIdx.x < 6) wg_ctl.ctr[threadIdx.x] = 0u;
-        if (wv == 0) prim();
+        if (wv == 0) {
+            prim();
+        } else if (wv == 1) {
+            const int ne = edge_list();
+            wg_ctl.nedges = ne;  // every lane stores the same value
+        }
         __syncthreads();
+        const int n_edges = (int)uni((uint32_t)wg_ctl.nedges);
         WG_MARK(1);
-        pass_dim1();
+        WG_COUNT(10, n_edges);
+        pass_dim1(n_edges);
         __syncthreads();
         WG_MARK(2);
         WG_COUNT(8, uni(wg_ctl.ctr[2]));
@@ -1093,7 +1086,7 @@ struct WgCx {
         WG_MARK(3);
         // the reduction ends with a barrier: the clearing marks are complete before the filter
         if (err == 0u) {
-            pass_dim2();
+            pass_dim2(n_edges);
             __syncthreads();
             WG_MARK(4);
             WG_COUNT(9, uni(wg_ctl.ctr[3]));
