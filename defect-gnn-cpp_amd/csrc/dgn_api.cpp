@@ -318,7 +318,8 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     HIP_TRY(c, W.atom_struct.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.cell_start.ensure(sizeof(int32_t) * (size_t)(A + B + 1)));
     HIP_TRY(c, W.cell_pos.ensure(sizeof(double4) * A1));
-    HIP_TRY(c, W.mask.ensure(sizeof(uint64_t) * kMaskWords * A1));
+    // hit masks: kMaskWords per atom, whole tiles (word-major per tile, graph_kernels.hip mask_index)
+    HIP_TRY(c, W.mask.ensure(sizeof(uint64_t) * kMaskWords * (size_t)std::max<int64_t>(nblocks * W.qa, 1)));
     // the Betti weights ride along with any pass that has species, so a Betti pass at the same
     // cutoff can reuse this one (betti_impl)
     const bool want_weight = b->species != nullptr;

@@ -704,10 +704,19 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
     __shared__ double4 offt_s[125];            \
     __shared__ uint32_t ring[kW][kRing];
 
+// Hit masks are stored per count tile of qa atoms, word-major ([tile][word][atom], kMaskWords
+// words reserved per atom): the tile's stores of word w are qa consecutive u64 (whole lines),
+// where an atom-major layout wrote each atom's nw <= kMaskWords words as a partial 64-byte sector
+// (read-modify-write at the ECC'd HBM: 0.46 GB of writes for 67 MB of masks per config-4 shard).
+__device__ __forceinline__ int64_t mask_index(int64_t gi, int wd, int qa) {
+    const int64_t t0 = gi - gi % qa;  // first atom of gi's tile
+    return t0 * kMaskWords + (int64_t)wd * qa + (gi - t0);
+}
+
 // ------------------------------------------------------------------------------------------
 // Kernel 1: per-atom kept counts + per-block (sum, max candidates, sum (m+1)^2, max structure
 // size). No atomics. For staged one-image structures it also records each query's exact hits as
-// a bit per atom (mask[gi][kMaskWords]) so the emit and Betti passes skip the search.
+// a bit per atom (word-major per tile, mask_index) so the emit and Betti passes skip the search.
 // ------------------------------------------------------------------------------------------
 #ifndef DGN_COUNT_WAVES
 #define DGN_COUNT_WAVES 5
@@ -765,8 +774,8 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     for (int i = threadIdx.x; i < nq; i += kGraphBlock) counts[g0 + i] = cnt_s[i];
     if (mask_out)
         for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock) {
-            const int a_ = x / kMaskWords, wd = x % kMaskWords;
-            if (wd < nw_s[a_]) mask_out[(g0 + a_) * kMaskWords + wd] = mask_s[a_][wd];
+            const int wd = x / nq, a_ = x - wd * nq;  // word-major: consecutive threads, consecutive atoms
+            if (wd < nw_s[a_]) mask_out[g0 * kMaskWords + (int64_t)wd * qa + a_] = mask_s[a_][wd];
         }
     if (threadIdx.x == 0) {
         int64_t s = 0;
@@ -1366,8 +1375,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     // the count pass's hit masks of the block's atoms (staged one-image structures)
     if (g.mask)
         for (int x = threadIdx.x; x < nq * nwm; x += kGraphBlock) {
-            const int a_ = x / nwm, wd = x - a_ * nwm;
-            mask_s[x] = g.mask[(g0 + a_) * kMaskWords + wd];
+            const int wd = x / nq, a_ = x - wd * nq;  // coalesced: consecutive threads, consecutive atoms
+            mask_s[a_ * nwm + wd] = g.mask[mask_index(g0 + a_, wd, qa)];
         }
     __syncthreads();
     EMIT_STAMP(0);
@@ -1532,8 +1541,10 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
     const int64_t g0 = first + (int64_t)blockIdx.x * kQA;
     const int nq = (int)(first + count - g0 < kQA ? first + count - g0 : kQA);
     if (g.mask) {
-        for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock)
-            mask_s[x / kMaskWords][x % kMaskWords] = g.mask[g0 * kMaskWords + x];
+        for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock) {
+            const int wd = x / nq, a_ = x - wd * nq;
+            mask_s[a_][wd] = g.mask[mask_index(g0 + a_, wd, g.qa)];
+        }
         __syncthreads();
     }
     for_block_atoms(g, st, first, first + count, blockIdx.x, kQA, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int, int64_t b) __attribute__((always_inline)) {

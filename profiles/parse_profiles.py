@@ -68,7 +68,8 @@ def main():
             cfg = gb.get("config", {})
             roof = summary.get("trace_bench", {}).get("roofline") or {}
             # must match bench.py's workload_key for the default run
-            key = "fcc4x%d_rc5.0_k20_nb50" % cfg.get("structures_per_gpu", 0) if cfg else None
+            rbf = "f32" if "RBF 50xf32" in cfg.get("workload", "") else "f64"
+            key = "fcc4x%d_rc5.0_k20_nb50_%s" % (cfg.get("structures_per_gpu", 0), rbf) if cfg else None
             path = sum(v["hbm_bytes_per_launch"] for v in per_kernel.values())
             summary["graph_path_pmc"] = {"per_kernel": per_kernel, "hbm_bytes_per_path": path,
                                          "algorithmic_bytes_per_path": roof.get("algorithmic_bytes_per_launch"),
