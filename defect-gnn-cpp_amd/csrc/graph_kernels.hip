@@ -705,9 +705,8 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
     __shared__ uint32_t ring[kW][kRing];
 
 // Hit masks are stored per count tile of qa atoms, word-major ([tile][word][atom], kMaskWords
-// words reserved per atom): the tile's stores of word w are qa consecutive u64 (whole lines),
-// where an atom-major layout wrote each atom's nw <= kMaskWords words as a partial 64-byte sector
-// (read-modify-write at the ECC'd HBM: 0.46 GB of writes for 67 MB of masks per config-4 shard).
+// words reserved per atom): the tile's stores of word w are qa consecutive u64 (whole lines; an
+// atom-major layout wrote each atom's nw <= kMaskWords words as half of a 64-byte sector).
 __device__ __forceinline__ int64_t mask_index(int64_t gi, int wd, int qa) {
     const int64_t t0 = gi - gi % qa;  // first atom of gi's tile
     return t0 * kMaskWords + (int64_t)wd * qa + (gi - t0);
