@@ -378,9 +378,11 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     GraphWork& W = c->gw;
     if (!W.have || W.pos != b->positions || W.atoms != b->num_atoms)
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
-    const int cap = graph_emit_cap(W.max_candidates);
+    const int cap = graph_emit_cap(W.max_candidates, W.k);
     if (cap == 0)
-        return fail(c, DGN_ERR_UNSUPPORTED, "more than 1024 neighbour candidates for one atom (cutoff too large)");
+        return fail(c, DGN_ERR_UNSUPPORTED,
+                    W.max_candidates > 2048 ? "more than 2048 neighbour candidates for one atom (cutoff too large)"
+                                            : "more than 1024 neighbour candidates for one atom needs max_neighbors <= 64");
     if (b->num_atoms == 0) return DGN_OK;
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, sizeof(uint32_t), c->stream));

@@ -79,7 +79,7 @@ inline int graph_tile_atoms(int64_t num_atoms, int cus) {
     while (qa > 4 && graph_blocks(num_atoms, qa) < 8 * (int64_t)cus) qa >>= 1;
     return qa;
 }
-int graph_emit_cap(uint32_t max_candidates);  // 0 if unsupported
+int graph_emit_cap(uint32_t max_candidates, uint64_t kmax);  // 0 if unsupported
 
 // ---- Betti ----
 struct BettiLaunch {

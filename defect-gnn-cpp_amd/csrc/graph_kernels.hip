@@ -1704,12 +1704,16 @@ hipError_t launch_block_scan(hipStream_t s, int64_t* v, const uint64_t* aux, int
     return hipGetLastError();
 }
 
-int graph_emit_cap(uint32_t m) {
+int graph_emit_cap(uint32_t m, uint64_t kmax) {
     if (m <= 64) return 64;
     if (m <= 128) return 128;
     if (m <= 256) return 256;
     if (m <= 512) return 512;
     if (m <= 1024) return 1024;
+    // 1,025..2,048 candidates (cutoffs up to ~20 A at FCC density): the streamed emit only
+    // (max_neighbors <= kStreamMaxK); the per-atom RBF layout would need a sorted-distance buffer
+    // per wave past the LDS
+    if (m <= 2048 && kmax <= (uint64_t)kStreamMaxK) return 2048;
     return 0;
 }
 
@@ -1805,6 +1809,10 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
         DGN_EMIT(256)
         DGN_EMIT(512)
         DGN_EMIT(1024)
+        case 2048:  // streamed emit only (graph_emit_cap)
+            if (!stream) return hipErrorInvalidValue;
+            launch_emit_t<2048, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
+            break;
         default:
             return hipErrorInvalidValue;
     }

@@ -158,6 +158,23 @@ def test_device_count_emit_full_shard(ctx):
         check_rbf(rbf[a:b], nl["dist"], 5.0, 0.1)
 
 
+def test_fcc256_cutoff_17A_above_1024_candidates(ctx):
+    """NeighborList(rc = 17, K = 20): ~1,200 candidates per atom (the 2,048-candidate streamed
+    emit), CSR bit-exact; the same cutoff without a neighbour cap (per-atom RBF rows) is outside the
+    envelope and fails loudly."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    p = abi.graph_params(r_cutoff=17.0, max_neighbors=20, rbf_cutoff=17.0, rbf_dr=0.1, write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, 17.0, 20)
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
+    check_rbf(g["rbf"], dist, 17.0, 0.1)
+    with pytest.raises(Exception):
+        ctx.host_graph(batch, abi.graph_params(r_cutoff=17.0, max_neighbors=None, rbf_cutoff=5.0, rbf_dr=0.1))
+
+
 @pytest.mark.parametrize("k", [20, None])
 def test_fcc256_cutoff_12A_above_512_candidates(ctx, k):
     """NeighborList(rc = 12): ~580 candidates per atom (the 1,024-candidate emit), CSR bit-exact."""
