@@ -61,6 +61,17 @@ __device__ __forceinline__ uint64_t uniw64(uint64_t x) {
     return ((uint64_t)uniw((uint32_t)(x >> 32)) << 32) | uniw((uint32_t)x);
 }
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// lane-to-lane hand-off through this wave's global scratch in the reduction's hot loop (V list,
+// pivot table, V store). The default is the workgroup barrier (its fence waits for every
+// outstanding global access of the wave, vmcnt(0)); -DDGN_WIDE_WAVE_FENCE uses a wavefront-scope
+// fence instead (A/B: a wave's own vector memory accesses are kept in order)
+__device__ __forceinline__ void wave_scratch_sync() {
+#ifdef DGN_WIDE_WAVE_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#else
+    __syncthreads();
+#endif
+}
 
 // combinatorial index of a packed simplex with nv vertices
 // insert vertex x (not in p) into a packed simplex of nv vertices
@@ -626,7 +637,7 @@ struct WideCx {
                     HM[slot] = meta;
                     sp<uint32_t>(ly.h_used)[npiv] = slot;
                 }
-                __syncthreads();  // the next lookups (other lanes) see it
+                wave_scratch_sync();  // the next lookups (other lanes) see it
                 return true;
             }
         }
@@ -764,7 +775,7 @@ struct WideCx {
             if (lane_id() == 0) VL[v] = x;
             v = v + 1;
         }
-        __syncthreads();  // the list (scratch) is read by every lane next
+        wave_scratch_sync();  // the list (scratch) is read by every lane next
         return true;
     }
 
@@ -957,7 +968,7 @@ struct WideCx {
                 }
                 const uint32_t* VL = sp<uint32_t>(ly.vlist);
                 for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
-                __syncthreads();
+                wave_scratch_sync();
                 m = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;
             }
