@@ -36,7 +36,7 @@ $(BUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp
+$(BUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp $(CSRC)/dgn_device.hpp
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
@@ -58,7 +58,7 @@ diag: $(DIAG)
 $(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 	@mkdir -p $(DBUILD)
 	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -c $< -o $@
-$(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp
+$(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp $(CSRC)/dgn_device.hpp
 	@mkdir -p $(DBUILD)
 	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -x hip -c $< -o $@
 $(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/betti_wg.o $(DBUILD)/betti_rank.o $(DBUILD)/node_kernels.o $(DBUILD)/dgn_api.o

@@ -82,7 +82,7 @@ struct Scalars {  // device-side scalars, one allocation
 
 // one neighbour pass's device workspace and the facts its count recorded (count -> emit handshake)
 struct GraphWork {
-    DevBuf meta, counts, block_sums, block_aux, atom_struct, cell_start, cell_pos, mask, weight;
+    DevBuf meta, counts, block_sums, block_aux, atom_struct, cell_start, cell_pos, mask, weight, defer;
     bool have = false;
     bool has_weight = false;  // weight[] holds the 1/count(species) Betti weights of this batch
     const double* pos = nullptr;
@@ -315,6 +315,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     HIP_TRY(c, W.counts.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
     HIP_TRY(c, W.block_aux.ensure(4 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, W.defer.ensure((size_t)std::max<int64_t>(nblocks, 1)));  // a flag byte per count tile
     HIP_TRY(c, W.atom_struct.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.cell_start.ensure(sizeof(int32_t) * (size_t)(A + B + 1)));
     HIP_TRY(c, W.cell_pos.ensure(sizeof(double4) * A1));
@@ -342,7 +343,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
         // compulsory traffic: positions in, per-atom counts out (+ the structure metadata)
         TimedLaunch t(c, betti ? "betti_nl_count" : "graph_count", (double)A * (24 + 4) + (double)B * sizeof(StructMeta), 0);
         HIP_TRY(c, launch_graph_count(c->stream, g, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
-                                      W.block_aux.as<uint64_t>(), W.mask.as<uint64_t>()));
+                                      W.block_aux.as<uint64_t>(), W.mask.as<uint64_t>(), W.defer.as<uint8_t>()));
     }
     {
         TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 32, 0);

@@ -15,8 +15,8 @@ constexpr int kWave = 64;  // CDNA wavefront; never 32
 struct StructMeta {
     double L[9];     // lattice rows a, b, c (row-major)
     double R[9];     // inverse lattice; column k = reciprocal vector of fractional axis k
-    double h[3];     // rc * |column k of R|: |frac_k| bound of any vector shorter than rc
-    double H[3];     // h + 1e-9: the conservative fractional half-widths every search uses
+    double H[3];     // rc * |column k of R| + 1e-9: the conservative fractional half-widths every
+                     // search uses (|frac_k| bound of any vector shorter than rc, plus a margin)
     int64_t first;   // first atom (global index)
     int32_t natoms;  // atoms in the structure
     int32_t nref;    // reference image range: ceil(rc / min row norm) + 1 (neighbor_list.cpp:68-72)
@@ -25,6 +25,10 @@ struct StructMeta {
     int32_t nc[3];   // cells per fractional axis (cell list), each cell at least H_k wide
     int32_t diag;    // lattice rows are axis-aligned (a = (a0,0,0), b = (0,b1,0), c = (0,0,c2))
     double band;     // |d2_approx - d2| bound of the fixed-point nearest-image distance (x64 margin)
+    // the one-image count pass's packed-f32 prefilter (count_one_image): lattice * 2^-32 in f32 and
+    // the d2 window (rc^2 -+ its rigorous band) outside which the f32 value decides
+    float lf[9];
+    float lo32, hi32;
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }

@@ -55,9 +55,12 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
 // per-atom hit counts m (every neighbour within rc; the emit keeps min(m, kmax)); per block:
 // block_sums[b] = sum of min(m, kmax) and block_aux[4b] = max m, block_aux[4b+1] = sum over atoms
 // of (m + 1)^2, block_aux[4b+2] = largest structure, block_aux[4b+3] = sum of m;
-// mask_out (optional) [A][kMaskWords]: exact hits of staged one-image structures
+// mask_out (optional) [A][kMaskWords]: exact hits of staged one-image structures.
+// defer [nblocks] (optional, needs mask_out): the one-image count kernel runs first and flags the
+// tiles it cannot count for the general kernel
+constexpr int64_t kCountListGrid = 2048;  // blocks of the general count launch over the flags
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint64_t* block_aux, uint64_t* mask_out);
+                              uint64_t* block_aux, uint64_t* mask_out, uint8_t* defer = nullptr);
 hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t* block_aux, int64_t nblocks,
                              int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq,
                              uint32_t* max_natoms, unsigned long long* sum_m);

@@ -68,8 +68,7 @@ __global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict
     m.R[6] = c20 * id; m.R[7] = c21 * id; m.R[8] = c22 * id;
     bool one = true;
     for (int k = 0; k < 3; ++k) {
-        m.h[k] = rc * sqrt(m.R[k] * m.R[k] + m.R[3 + k] * m.R[3 + k] + m.R[6 + k] * m.R[6 + k]);
-        m.H[k] = m.h[k] + 1e-9;
+        m.H[k] = rc * sqrt(m.R[k] * m.R[k] + m.R[3 + k] * m.R[3 + k] + m.R[6 + k] * m.R[6 + k]) + 1e-9;
         one = one && m.H[k] < 0.5;
     }
     // Eigen Matrix3d row norm: x0 + (x1 + x2) (fixed-size unrolled redux), neighbor_list.cpp:69
@@ -92,6 +91,23 @@ __global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict
         double lsum = 0.0;
         for (int r = 0; r < 3; ++r) lsum += fabs(L[3 * r]) + fabs(L[3 * r + 1]) + fabs(L[3 * r + 2]);
         m.band = 64.0 * 2.0 * rc * lsum * 0x1p-31 + 1e-12 * rc * rc;
+    }
+    // the count pass's f32 window (count_one_image), once per structure instead of per query:
+    //   band32 bounds |approx - exact| for candidates with either value below rc^2 + band32: the
+    //   fixed-point quantisation (band), f32 displacement error eps <= 5 * 2^-24 * 0.5 * sum|L| per
+    //   axis (conversion of the 32-bit fraction, the rounded f32 lattice, product, two sums),
+    //   2 sqrt(3) R eps + 3 eps^2 on the square (R = rc + 1e-3 bounds |d|), 3 * 2^-24 R^2 for the
+    //   f32 square and sums, 2^-20 rc^2 for rounding the thresholds; the sum is doubled.
+    {
+        const double rc2 = rc * rc;
+        double lsum = 0.0;
+        for (int k = 0; k < 9; ++k) lsum += fabs(L[k]);
+        const double eps = 5.0 * 0x1p-24 * 0.5 * lsum, R = sqrt(rc2) + 1e-3;
+        const double band32 = 2.0 * (m.band + 2.0 * 1.7320508075688772 * R * eps + 3.0 * eps * eps +
+                                     3.0 * 0x1p-24 * R * R + 0x1p-20 * rc2);
+        m.lo32 = (float)(rc2 - band32);
+        m.hi32 = (float)(rc2 + band32);
+        for (int k = 0; k < 9; ++k) m.lf[k] = (float)(L[k] * 0x1p-32);
     }
     for (int k = 0; k < 3; ++k) m.nc[k] = 1;
     if (m.cells) {
@@ -282,18 +298,21 @@ struct PosSrc {
 // the kernel's own stores may alias it and re-loads every field with vector loads + waits.)
 __device__ __forceinline__ StructMeta load_meta_uniform(const StructMeta* p) {
     constexpr int N = (int)(sizeof(StructMeta) / 4);
-    static_assert(N <= kWave, "StructMeta must fit one wave load");
+    static_assert(N <= 2 * kWave, "StructMeta must fit two wave loads");
     const uint32_t* src = reinterpret_cast<const uint32_t*>(p);
     const int lane = lane_id();
     const uint32_t v = lane < N ? src[lane] : 0u;
+    const uint32_t v2 = N > kWave && lane + kWave < N ? src[lane + kWave] : 0u;
     StructMeta m;
     uint32_t* dst = reinterpret_cast<uint32_t*>(&m);
 #pragma unroll
-    for (int t = 0; t < N; ++t) dst[t] = (uint32_t)__builtin_amdgcn_readlane((int)v, t);
+    for (int t = 0; t < N; ++t) dst[t] = (uint32_t)__builtin_amdgcn_readlane((int)(t < kWave ? v : v2), t & (kWave - 1));
     return m;
 }
 
-template <class PerAtom>
+// POS = false: only the fixed-point coordinates (and offset table) are staged; positions stay in
+// global memory (graph_count_one_kernel, whose tiles hold staged one-image structures only)
+template <bool POS = true, class PerAtom>
 __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const StageView st, int64_t a_begin,
                                                 int64_t a_end, int64_t tile, int qa, PerAtom&& per_atom) {
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -313,9 +332,11 @@ __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const Stag
             const double* src = g.pos + 3 * first;
             for (int t = threadIdx.x; t < natoms; t += kGraphBlock) {
                 const double p[3] = {src[3 * t], src[3 * t + 1], src[3 * t + 2]};
-                st.x[t] = p[0];
-                st.y[t] = p[1];
-                st.z[t] = p[2];
+                if constexpr (POS) {
+                    st.x[t] = p[0];
+                    st.y[t] = p[1];
+                    st.z[t] = p[2];
+                }
                 if (M.one) {
                     int sf[3];
                     uint32_t W[3];
@@ -375,8 +396,11 @@ __device__ __forceinline__ void unpack_jimg(uint64_t key, int& j, int& na, int& 
 // nearest image — its only candidate image. Its image n = (s_q - s_j) - carry (s = floors, carry =
 // the wrap of W_j - W_q) and the reference arithmetic (offset from the staged 5^3 table, |n| <=
 // nref = 2) give the exact d2.
-__device__ __forceinline__ double exact_one(const StructMeta& M, const StageView& st, const u32x4 fq, const u32x4 fj,
-                                            int j, const double q[3], int n[3], bool& inr) {
+// posj(j, p) yields atom j's position (LDS stage or global memory: the same doubles)
+template <class PosJ>
+__device__ __forceinline__ double exact_one_at(const StructMeta& M, const DGN_LDS f64x4* offt, const u32x4 fq,
+                                               const u32x4 fj, PosJ&& posj, int j, const double q[3], int n[3],
+                                               bool& inr) {
     inr = true;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -388,17 +412,30 @@ __device__ __forceinline__ double exact_one(const StructMeta& M, const StageView
         inr = inr && (uint32_t)(n[k] + 2) <= 4u;  // |n| <= nref = 2
     }
     f64x4 o;
-    if (st.offt) {
-        o = st.offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
+    if (offt) {
+        o = offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
     } else {  // the table's arithmetic: ((na*a + nb*b) + nc*c)
         const double na = inr ? (double)n[0] : 0.0, nb = inr ? (double)n[1] : 0.0, nc = inr ? (double)n[2] : 0.0;
         o.x = (na * M.L[0] + nb * M.L[3]) + nc * M.L[6];
         o.y = (na * M.L[1] + nb * M.L[4]) + nc * M.L[7];
         o.z = (na * M.L[2] + nb * M.L[5]) + nc * M.L[8];
     }
-    const double p0 = st.x[j] + o.x, p1 = st.y[j] + o.y, p2 = st.z[j] + o.z;  // p = pos + offset
+    double pj[3];
+    posj(j, pj);
+    const double p0 = pj[0] + o.x, p1 = pj[1] + o.y, p2 = pj[2] + o.z;  // p = pos + offset
     const double e0 = q[0] - p0, e1 = q[1] - p1, e2 = q[2] - p2;
     return ((0.0 + e0 * e0) + e1 * e1) + e2 * e2;  // L2_Simple_Adaptor accumulation
+}
+__device__ __forceinline__ double exact_one(const StructMeta& M, const StageView& st, const u32x4 fq, const u32x4 fj,
+                                            int j, const double q[3], int n[3], bool& inr) {
+    return exact_one_at(
+        M, st.offt, fq, fj,
+        [&](int jj, double p[3]) __attribute__((always_inline)) {
+            p[0] = st.x[jj];
+            p[1] = st.y[jj];
+            p[2] = st.z[jj];
+        },
+        j, q, n, inr);
 }
 // |nearest-image displacement|^2 from the fixed-point coordinates (within M.band of the exact d2)
 __device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq, const u32x4 fj) {
@@ -421,33 +458,24 @@ __device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq,
 // lane from an approximate nearest-image distance computed for both at once in packed f32
 // (v_pk_fma_f32); only candidates within `band32` of rc^2 (a few per thousand queries) take the
 // exact reference test in f64. The self image (j == li, n = 0) is the only image of the query
-// atom within rc. Returns m; mask[t] = the hit ballot of atom tile t (a bit per atom).
-//   band32 bounds |approx - exact| for candidates with either value below rc^2 + band32: the
-//   fixed-point quantisation (M.band), f32 displacement error eps <= 5 * 2^-24 * 0.5 * sum|L| per
-//   axis (conversion of the 32-bit fraction, the rounded f32 lattice, product, two sums),
-//   2 sqrt(3) R eps + 3 eps^2 on the square (R = rc + 1e-3 bounds |d|), 3 * 2^-24 R^2 for the
-//   f32 square and sums, 2^-20 rc^2 for rounding the thresholds; the sum is doubled.
+// atom within rc. Returns m; mask[t] = the hit ballot of atom tile t (a bit per atom). The f32
+// lattice and the window [lo32, hi32] = rc^2 -+ band32 come from prep_meta_kernel (derivation
+// there).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ int count_staged_one(const StructMeta& M, const StageView st, const double q[3], int li,
-                                                double rc2, DGN_LDS uint64_t* mask_words) {
+template <class PosJ>
+__device__ __forceinline__ int count_one_image(const StructMeta& M, const DGN_LDS u32x4* fx, const DGN_LDS f64x4* offt,
+                                               PosJ&& posj, int li, double rc2, DGN_LDS uint64_t* mask_words) {
     const int lane = lane_id();
     const int natoms = M.natoms;
-    const u32x4 fq = st.fx[li];
-    double lsum = 0.0;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) lsum += fabs(M.L[k]);
-    const double eps = 5.0 * 0x1p-24 * 0.5 * lsum, R = sqrt(rc2) + 1e-3;
-    const double band32 =
-        2.0 * (M.band + 2.0 * 1.7320508075688772 * R * eps + 3.0 * eps * eps + 3.0 * 0x1p-24 * R * R + 0x1p-20 * rc2);
-    const float lo32 = (float)(rc2 - band32), hi32 = (float)(rc2 + band32);
-    float Lf[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) Lf[k] = (float)(M.L[k] * 0x1p-32);
+    const u32x4 fq = fx[li];
+    const float lo32 = M.lo32, hi32 = M.hi32;  // prep_meta_kernel (band32 derivation there)
+    const float* Lf = M.lf;
     int m = 0;
+#pragma nounroll
     for (int base = 0, t = 0; base < natoms; base += 2 * kWave, t += 2) {
         const int j0 = base + lane, j1 = base + kWave + lane;
-        const u32x4 a = st.fx[j0 < natoms ? j0 : natoms - 1];
-        const u32x4 c = st.fx[j1 < natoms ? j1 : natoms - 1];
+        const u32x4 a = fx[j0 < natoms ? j0 : natoms - 1];
+        const u32x4 c = fx[j1 < natoms ? j1 : natoms - 1];
         const f32x2 u0 = {(float)(int)(a.x - fq.x), (float)(int)(c.x - fq.x)};
         const f32x2 u1 = {(float)(int)(a.y - fq.y), (float)(int)(c.y - fq.y)};
         const f32x2 u2 = {(float)(int)(a.z - fq.z), (float)(int)(c.z - fq.z)};
@@ -464,16 +492,22 @@ __device__ __forceinline__ int count_staged_one(const StructMeta& M, const Stage
         const f32x2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
         const bool ok0 = j0 < natoms && j0 != li, ok1 = j1 < natoms && j1 != li;
         bool hit0 = ok0 && d2.x < lo32, hit1 = ok1 && d2.y < lo32;
-        if (ok0 && !hit0 && d2.x <= hi32) {  // borderline: the exact reference arithmetic decides
+        // borderline: the exact reference arithmetic decides (the query position is only read
+        // here, a few times per thousand queries)
+        if (ok0 && !hit0 && d2.x <= hi32) {
             int n[3];
             bool inr;
-            const double e2 = exact_one(M, st, fq, a, j0, q, n, inr);
+            double q[3];
+            posj(li, q);
+            const double e2 = exact_one_at(M, offt, fq, a, posj, j0, q, n, inr);
             hit0 = inr && e2 < rc2;
         }
         if (ok1 && !hit1 && d2.y <= hi32) {
             int n[3];
             bool inr;
-            const double e2 = exact_one(M, st, fq, c, j1, q, n, inr);
+            double q[3];
+            posj(li, q);
+            const double e2 = exact_one_at(M, offt, fq, c, posj, j1, q, n, inr);
             hit1 = inr && e2 < rc2;
         }
         const uint64_t bal0 = ballot(hit0), bal1 = ballot(hit1);
@@ -484,6 +518,17 @@ __device__ __forceinline__ int count_staged_one(const StructMeta& M, const Stage
         m += __popcll(bal0) + __popcll(bal1);
     }
     return m;
+}
+__device__ __forceinline__ int count_staged_one(const StructMeta& M, const StageView st, int li, double rc2,
+                                                DGN_LDS uint64_t* mask_words) {
+    return count_one_image(
+        M, st.fx, st.offt,
+        [&](int jj, double p[3]) __attribute__((always_inline)) {
+            p[0] = st.x[jj];
+            p[1] = st.y[jj];
+            p[2] = st.z[jj];
+        },
+        li, rc2, mask_words);
 }
 
 // Hit collection on a staged one-image structure (emit / Betti): `produce(base, lane, fq) -> bool`
@@ -714,83 +759,184 @@ __device__ __forceinline__ int64_t mask_index(int64_t gi, int wd, int qa) {
 
 // ------------------------------------------------------------------------------------------
 // Kernel 1: per-atom kept counts + per-block (sum, max candidates, sum (m+1)^2, max structure
-// size). No atomics. For staged one-image structures it also records each query's exact hits as
-// a bit per atom (word-major per tile, mask_index) so the emit and Betti passes skip the search.
+// size). No atomics on the data. For staged one-image structures it also records each query's
+// exact hits as a bit per atom (word-major per tile, mask_index) so the emit and Betti passes
+// skip the search. Two kernels (launch_graph_count):
+//   1a graph_count_one_kernel, every tile: tiles whose structures are all staged one-image ones
+//      (cells wider than 2 rc, <= kStage atoms: config 4's FCC-256 at 5 A) are counted here; any
+//      other tile is flagged and left alone;
+//   1b graph_count_kernel over the flagged tiles (every search strategy).
+// 1a stages only the fixed-point coordinates (16 B per atom) and the image-offset table; the rare
+// borderline exact test reads positions from global memory. Without the general / cell-list
+// search code in the kernel it needs no spills and ~16 KB of LDS, where the combined kernel held
+// 96 VGPRs + 12 spilled (0.45 GB of scratch writes per config-4 shard) and 29 KB of LDS.
 // ------------------------------------------------------------------------------------------
 #ifndef DGN_COUNT_WAVES
 #define DGN_COUNT_WAVES 5
 #endif
-__global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT_WAVES))) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
-                                                                   int64_t* __restrict__ block_sums,
-                                                                   uint64_t* __restrict__ block_aux,
-                                                                   uint64_t* __restrict__ mask_out) {
-    __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
-    DGN_SEARCH_SMEM
-    __shared__ int32_t cnt_s[kQA], nw_s[kQA];        // block outputs, written at the end (no global
-    __shared__ uint64_t mask_s[kQA][kMaskWords];     // memory inside the per-query loop)
-    __shared__ int64_t wsum[kW];
-    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW], wm[kW];
-    const StageView st = make_stage(stage_mem, kStage, offt_s);
+#ifndef DGN_COUNT1_WAVES
+#define DGN_COUNT1_WAVES 8
+#endif
+
+// the per-wave statistics of one tile, combined and stored with the tile's counts and masks
+struct CountTileOut {
+    DGN_LDS int32_t* cnt;            // [qa] hits per query
+    DGN_LDS int32_t* nw;             // [qa] mask words per query (0: no mask)
+    DGN_LDS uint64_t (*mask)[kMaskWords];
+    DGN_LDS int64_t* wsum;           // [kW] per-wave sums ...
+    DGN_LDS uint64_t *wmax, *wsq, *wnat, *wm;
+};
+struct CountAcc {
+    int64_t sum = 0;
+    uint32_t max = 0, nat = 0;
+    uint64_t sq = 0, m = 0;
+    __device__ __forceinline__ void add(int m_, int natoms, uint64_t kmax) {
+        sum += (uint64_t)m_ < kmax ? (int64_t)m_ : (int64_t)kmax;
+        m += (uint64_t)m_;
+        max = (uint32_t)m_ > max ? (uint32_t)m_ : max;
+        nat = (uint32_t)natoms > nat ? (uint32_t)natoms : nat;
+        sq += (uint64_t)(m_ + 1) * (uint64_t)(m_ + 1);  // local-complex n^2
+    }
+};
+__device__ __forceinline__ void count_tile_store(const GraphLaunch& g, int64_t tile, const CountAcc& acc,
+                                                 const CountTileOut& o, int32_t* __restrict__ counts,
+                                                 int64_t* __restrict__ block_sums, uint64_t* __restrict__ block_aux,
+                                                 uint64_t* __restrict__ mask_out) {
     const int w = threadIdx.x / kWave;
-    const int lane = lane_id();
     const int qa = g.qa;
-    const int64_t g0 = (int64_t)blockIdx.x * qa;
-    int64_t my_sum = 0;
-    uint32_t my_max = 0, my_nat = 0;
-    uint64_t my_sq = 0, my_m = 0;
-    for_block_atoms(g, st, 0, g.num_atoms, blockIdx.x, qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
-        const int li = (int)(gi - M.first);
-        double q[3];
-        P.get(li, q);
-        int m = 0, nw = 0;
-        if (M.one && P.staged) {
-            m = count_staged_one(M, P.st, q, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr);
-            nw = mask_out ? (M.natoms + 63) / 64 : 0;
-        } else {
-            search(g, M, b, P, q, li, lds(ring[w]), nullptr,
-                   [&](bool hit, int, int, int, int, double) { m += __popcll(ballot(hit)); });
-        }
-        const int64_t c = (uint64_t)m < g.kmax ? (int64_t)m : (int64_t)g.kmax;
-        if (lane == 0) {
-            cnt_s[t] = (int32_t)m;  // every hit: the emit keeps min(m, kmax), a Betti pass at this rc reuses m
-            nw_s[t] = nw;
-        }
-        my_sum += c;
-        my_m += (uint64_t)m;
-        my_max = (uint32_t)m > my_max ? (uint32_t)m : my_max;
-        my_nat = (uint32_t)M.natoms > my_nat ? (uint32_t)M.natoms : my_nat;
-        my_sq += (uint64_t)(m + 1) * (uint64_t)(m + 1);  // local-complex n^2
-    });
-    if (lane == 0) {
-        wsum[w] = my_sum;
-        wmax[w] = my_max;
-        wsq[w] = my_sq;
-        wnat[w] = my_nat;
-        wm[w] = my_m;
+    const int64_t g0 = tile * qa;
+    if (lane_id() == 0) {
+        o.wsum[w] = acc.sum;
+        o.wmax[w] = acc.max;
+        o.wsq[w] = acc.sq;
+        o.wnat[w] = acc.nat;
+        o.wm[w] = acc.m;
     }
     __syncthreads();
     const int nq = (int)(g.num_atoms - g0 < qa ? g.num_atoms - g0 : qa);
-    for (int i = threadIdx.x; i < nq; i += kGraphBlock) counts[g0 + i] = cnt_s[i];
+    for (int i = threadIdx.x; i < nq; i += kGraphBlock) counts[g0 + i] = o.cnt[i];
     if (mask_out)
         for (int x = threadIdx.x; x < nq * kMaskWords; x += kGraphBlock) {
             const int wd = x / nq, a_ = x - wd * nq;  // word-major: consecutive threads, consecutive atoms
-            if (wd < nw_s[a_]) mask_out[g0 * kMaskWords + (int64_t)wd * qa + a_] = mask_s[a_][wd];
+            if (wd < o.nw[a_]) mask_out[g0 * kMaskWords + (int64_t)wd * qa + a_] = o.mask[a_][wd];
         }
     if (threadIdx.x == 0) {
         int64_t s = 0;
         uint64_t mx = 0, sq = 0, nat = 0, sm = 0;
         for (int k = 0; k < kW; ++k) {
-            s += wsum[k];
-            sm += wm[k];
-            mx = wmax[k] > mx ? wmax[k] : mx;
-            nat = wnat[k] > nat ? wnat[k] : nat;
-            sq += wsq[k];
+            s += o.wsum[k];
+            sm += o.wm[k];
+            mx = o.wmax[k] > mx ? o.wmax[k] : mx;
+            nat = o.wnat[k] > nat ? o.wnat[k] : nat;
+            sq += o.wsq[k];
         }
-        block_sums[blockIdx.x] = s;
-        block_aux[4 * blockIdx.x] = mx;
-        block_aux[4 * blockIdx.x + 1] = sq;
-        block_aux[4 * blockIdx.x + 2] = nat;
-        block_aux[4 * blockIdx.x + 3] = sm;
+        block_sums[tile] = s;
+        block_aux[4 * tile] = mx;
+        block_aux[4 * tile + 1] = sq;
+        block_aux[4 * tile + 2] = nat;
+        block_aux[4 * tile + 3] = sm;
+    }
+}
+
+#define DGN_COUNT_SMEM                                                                   \
+    __shared__ int32_t cnt_s[kQA], nw_s[kQA]; /* block outputs, written at the end */    \
+    __shared__ uint64_t mask_s[kQA][kMaskWords];                                         \
+    __shared__ int64_t wsum[kW];                                                         \
+    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW], wm[kW];                             \
+    const CountTileOut out{lds(cnt_s), lds(nw_s), reinterpret_cast<DGN_LDS uint64_t(*)[kMaskWords]>(lds(&mask_s[0][0])), \
+                           lds(wsum), lds(wmax), lds(wsq), lds(wnat), lds(wm)};
+
+__global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT1_WAVES))) void graph_count_one_kernel(
+    GraphLaunch g, int32_t* __restrict__ counts, int64_t* __restrict__ block_sums, uint64_t* __restrict__ block_aux,
+    uint64_t* __restrict__ mask_out, uint8_t* __restrict__ defer) {
+    __shared__ u32x4 fx_s[kStage];
+    __shared__ double4 offt_s[125];
+    DGN_COUNT_SMEM
+    const int lane = lane_id();
+    const int64_t tile = blockIdx.x;
+    const int64_t g0 = tile * g.qa;
+    const int64_t g1 = g0 + g.qa < g.num_atoms ? g0 + g.qa : g.num_atoms;
+    // every structure of the tile staged and one-image? (wave-uniform: metadata in SGPRs)
+    bool one = true;
+    for (int32_t b = uni_i32(g.atom_struct[g0]), bl = uni_i32(g.atom_struct[g1 - 1]); b <= bl && one; ++b) {
+        const StructMeta M = load_meta_uniform(g.meta + b);
+        one = M.natoms == 0 || (M.one && M.natoms <= kStage);
+    }
+    if (threadIdx.x == 0) defer[tile] = one ? 0 : 1;  // every tile's flag is written: no memset
+    if (!one) return;
+    // stage view without positions (for_block_atoms<false> stores fx and the offset table only)
+    const StageView st{nullptr, nullptr, nullptr, lds(fx_s), reinterpret_cast<DGN_LDS f64x4*>(lds(offt_s)), kStage};
+    CountAcc acc;
+    for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t) __attribute__((always_inline)) {
+        const int li = (int)(gi - M.first);
+        const double* gp = P.gpos;
+        const int m = count_one_image(
+            M, st.fx, st.offt,
+            [&](int jj, double p[3]) __attribute__((always_inline)) {
+                p[0] = gp[3 * jj];
+                p[1] = gp[3 * jj + 1];
+                p[2] = gp[3 * jj + 2];
+            },
+            li, g.rc2, lds(mask_s[t]));
+        if (lane == 0) {
+            cnt_s[t] = (int32_t)m;
+            nw_s[t] = (M.natoms + 63) / 64;
+        }
+        acc.add(m, M.natoms, g.kmax);
+    });
+    count_tile_store(g, tile, acc, out, counts, block_sums, block_aux, mask_out);
+}
+
+// defer: graph_count_one_kernel's per-tile flags (the grid strides over the tiles: lane k of every
+// wave loads the flag of tile blockIdx.x + k * gridDim.x of the current round, the ballot lists the
+// block's deferred tiles), or null: tile = blockIdx.x (no 1a pass, e.g. without hit masks)
+__global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT_WAVES))) void graph_count_kernel(GraphLaunch g, int32_t* __restrict__ counts,
+                                                                   int64_t* __restrict__ block_sums,
+                                                                   uint64_t* __restrict__ block_aux,
+                                                                   uint64_t* __restrict__ mask_out,
+                                                                   const uint8_t* __restrict__ defer) {
+    __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
+    DGN_SEARCH_SMEM
+    DGN_COUNT_SMEM
+    const StageView st = make_stage(stage_mem, kStage, offt_s);
+    const int w = threadIdx.x / kWave;
+    const int lane = lane_id();
+    auto run_tile = [&](int64_t tile) __attribute__((always_inline)) {
+        CountAcc acc;
+        for_block_atoms(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b) __attribute__((always_inline)) {
+            const int li = (int)(gi - M.first);
+            int m = 0, nw = 0;
+            if (M.one && P.staged) {
+                m = count_staged_one(M, P.st, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr);
+                nw = mask_out ? (M.natoms + 63) / 64 : 0;
+            } else {
+                double q[3];
+                P.get(li, q);
+                search(g, M, b, P, q, li, lds(ring[w]), nullptr,
+                       [&](bool hit, int, int, int, int, double) { m += __popcll(ballot(hit)); });
+            }
+            if (lane == 0) {
+                cnt_s[t] = (int32_t)m;  // every hit: the emit keeps min(m, kmax), a Betti pass at this rc reuses m
+                nw_s[t] = nw;
+            }
+            acc.add(m, M.natoms, g.kmax);
+        });
+        count_tile_store(g, tile, acc, out, counts, block_sums, block_aux, mask_out);
+        __syncthreads();  // the next tile reuses the block's LDS outputs
+    };
+    if (!defer) {
+        run_tile(blockIdx.x);
+        return;
+    }
+    const int64_t nt = (g.num_atoms + g.qa - 1) / g.qa, G = gridDim.x;
+    for (int64_t base = blockIdx.x; base < nt; base += (int64_t)kWave * G) {
+        const int64_t mine = base + (int64_t)lane * G;
+        uint64_t bal = ballot(mine < nt && defer[mine] != 0);  // the same in every wave of the block
+        while (bal) {
+            const int k = __builtin_ctzll(bal);
+            bal &= bal - 1;
+            run_tile(base + (int64_t)k * G);
+        }
     }
 }
 
@@ -1688,11 +1834,21 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
 }
 
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
-                              uint64_t* block_aux, uint64_t* mask_out) {
+                              uint64_t* block_aux, uint64_t* mask_out, uint8_t* defer) {
     const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
-    hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
-                       block_aux, mask_out);
+    if (!mask_out || !defer) {
+        hipLaunchKernelGGL(graph_count_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
+                           block_aux, mask_out, (const uint8_t*)nullptr);
+        return hipGetLastError();
+    }
+    // 1a over every tile, then 1b over the tiles 1a flagged (a fixed grid strides over the flags,
+    // so a launch with nothing deferred costs one short launch and no host read)
+    hipLaunchKernelGGL(graph_count_one_kernel, dim3((unsigned)nb), dim3(kGraphBlock), 0, s, g, counts, block_sums,
+                       block_aux, mask_out, defer);
+    const unsigned grid = (unsigned)(nb < kCountListGrid ? nb : kCountListGrid);
+    hipLaunchKernelGGL(graph_count_kernel, dim3(grid), dim3(kGraphBlock), 0, s, g, counts, block_sums, block_aux,
+                       mask_out, (const uint8_t*)defer);
     return hipGetLastError();
 }
 
