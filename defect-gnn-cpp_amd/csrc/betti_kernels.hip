@@ -207,6 +207,7 @@ struct Complex {
     int n_d0, n_inf0, n_p1, n_p2;
     int n_adds, n_spills;  // diagnostics
 #ifdef DGN_PHASE_TIMING
+    mutable uint32_t walk_steps = 0;  // min-cofacet walk steps of this lane (lane efficiency)
     uint64_t* ph = nullptr;
     uint64_t* tprev = nullptr;
     __device__ void stamp(int k) {
@@ -282,6 +283,9 @@ struct Complex {
         const uint32_t* rcv = Db() + c * S;
         // four candidates per step (descending), their distance reads issued together
         while (cand) {
+#ifdef DGN_PHASE_TIMING
+            ++walk_steps;
+#endif
             int kk[4];
             bool val[4];
 #pragma unroll
@@ -997,19 +1001,35 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     int next_edge = 0;
                     int ea = 0, eb = 0;
                     uint64_t tmask = 0;
+                    // the edge list is read through a register window: lane t holds edges wbase + t
+                    // (win) and wbase + 64 + t (win_next, loaded one window ahead), so a refill is a
+                    // lane shuffle instead of a dependent scratch load (edges without a c < b in
+                    // common refill again at once)
+                    int wbase = 0;
+                    uint32_t win = lane < n_edges ? (uint32_t)edges[lane] : 0u;
+                    uint32_t win_next = kWave + lane < n_edges ? (uint32_t)edges[kWave + lane] : 0u;
                     while (true) {
                         while (true) {  // refill lanes with empty masks
                             const bool need = tmask == 0;
                             const uint64_t bal = ballot(need);
                             if (!bal || next_edge >= n_edges) break;
                             const int e = next_edge + mask_prefix(bal);
+                            const int off = e - wbase;  // < 128: next_edge - wbase < 64
+                            const uint32_t v0 = (uint32_t)__shfl((int)win, off & (kWave - 1), kWave);
+                            const uint32_t v1 = (uint32_t)__shfl((int)win_next, off & (kWave - 1), kWave);
                             if (need && e < n_edges) {
-                                const uint32_t ed = edges[e];
+                                const uint32_t ed = off < kWave ? v0 : v1;
                                 ea = ed >> 8;
                                 eb = ed & 255;
                                 tmask = s.adj[ea] & s.adj[eb] & ((1ull << eb) - 1ull);
                             }
                             next_edge += __popcll(bal);
+                            if (next_edge - wbase >= kWave) {  // window consumed: slide by 64
+                                wbase += kWave;
+                                win = win_next;
+                                const int t = wbase + kWave + lane;
+                                win_next = t < n_edges ? (uint32_t)edges[t] : 0u;
+                            }
                             if (ballot(tmask == 0) == 0) break;
                         }
                         const bool active = tmask != 0;
@@ -1068,6 +1088,20 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         }
                         mincof[tri_dense(a, b, c)] = (uint8_t)mc;
                     }
+#ifdef DGN_PHASE_TIMING
+                    // lane efficiency of the round-synchronous walk: steps summed over lanes [29],
+                    // the longest lane's steps [30], rounds [31]
+                    {
+                        const uint32_t st_ = cx.walk_steps;
+                        cx.walk_steps = 0;
+                        const uint64_t tot_ = wave_sum((uint64_t)st_), mx_ = wave_max((uint64_t)st_);
+                        if (lane == 0) {
+                            ph[29] += tot_;
+                            ph[30] += mx_;
+                            ph[31] += 1;
+                        }
+                    }
+#endif
                     cx.append_pairs(2, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {

@@ -44,5 +44,7 @@ out = {"kind": kind, "m": m, "B": B, "rc": rc, "atoms": A, "host_betti_s": round
        "pivot_V_entries_per_complex": ph[14] / A, "pivot_V_sq_per_complex": ph[15] / A,
        "max_V": ph[23], "pivot_iters_per_complex": ph[24] / A, "pivot_iter_entries_per_complex": ph[25] / A,
        "trivial_columns_per_complex": ph[27] / A, "zero_columns_per_complex": ph[28] / A,
-       "dim2_enumerate_cycles_per_complex": round(ph[26] / A), "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
+       "dim2_enumerate_cycles_per_complex": round(ph[26] / A),
+       "dim2_walk_steps_per_complex": ph[29] / A, "dim2_rounds_per_complex": ph[31] / A,
+       "dim2_walk_lane_efficiency": ph[29] / max(1, 64 * ph[30]), "serial_sub_cycles_per_complex": {n: round(ph[16 + i] / A) for i, n in enumerate(sub)}}
 print(json.dumps(out, indent=1))
