@@ -867,9 +867,19 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     // stage view without positions (for_block_atoms<false> stores fx and the offset table only)
     const StageView st{nullptr, nullptr, nullptr, lds(fx_s), reinterpret_cast<DGN_LDS f64x4*>(lds(offt_s)), kStage};
     CountAcc acc;
+#if defined(DGN_COUNT1_PROBE) && DGN_COUNT1_PROBE == 2
+    // diagnostics builds only (tools/count_probe.py; wrong counts): no staging, no search
+    if (threadIdx.x < g.qa) cnt_s[threadIdx.x] = 0, nw_s[threadIdx.x] = 0;
+    __syncthreads();
+#else
     for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         const double* gp = P.gpos;
+#if defined(DGN_COUNT1_PROBE) && DGN_COUNT1_PROBE == 1
+        // diagnostics builds only: staging without the search
+        const int m = (int)st.fx[li].x & 1;
+        (void)gp;
+#else
         const int m = count_one_image(
             M, st.fx, st.offt,
             [&](int jj, double p[3]) __attribute__((always_inline)) {
@@ -878,12 +888,14 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
                 p[2] = gp[3 * jj + 2];
             },
             li, g.rc2, lds(mask_s[t]));
+#endif
         if (lane == 0) {
             cnt_s[t] = (int32_t)m;
             nw_s[t] = (M.natoms + 63) / 64;
         }
         acc.add(m, M.natoms, g.kmax);
     });
+#endif
     count_tile_store(g, tile, acc, out, counts, block_sums, block_aux, mask_out);
 }
 
