@@ -28,3 +28,22 @@ def ctx():
     c = dgn.Context(0)
     yield c
     c.close()
+
+
+def mixed_batch(npairs):
+    """FCC-256 cells (one image per axis at rc 5: the one-image count kernel) alternating with
+    SC-64 cells (L = 9.28 A < 2 rc: the general search), so count tiles are one-image, general or
+    straddle both (flagged for the general count kernel)."""
+    import numpy as np
+    import dgn
+
+    f, s = dgn.synth_batch("fcc", 4, npairs), dgn.synth_batch("sc", 4, npairs)
+    fo, so = f["atom_offset"], s["atom_offset"]
+    lat, pos, spc, sizes = [], [], [], []
+    for i in range(npairs):
+        lat += [f["lattice"][i], s["lattice"][i]]
+        pos += [f["positions"][fo[i]:fo[i + 1]], s["positions"][so[i]:so[i + 1]]]
+        spc += [f["species"][fo[i]:fo[i + 1]], s["species"][so[i]:so[i + 1]]]
+        sizes += [fo[i + 1] - fo[i], so[i + 1] - so[i]]
+    return {"lattice": np.stack(lat), "positions": np.concatenate(pos), "species": np.concatenate(spc).astype(np.int32),
+            "atom_offset": np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)}

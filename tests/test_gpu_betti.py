@@ -5,7 +5,7 @@ import os
 
 import numpy as np
 import pytest
-from conftest import GOLDEN
+from conftest import GOLDEN, mixed_batch
 
 import dgn
 import oracle_py as O
@@ -80,6 +80,19 @@ def test_fcc256_batch_vs_oracle(ctx):
     n = 256
     for s in range(3):
         sl = slice(s * n, (s + 1) * n)
+        fo, co = O.structure_betti(batch["lattice"][s], batch["positions"][sl], batch["species"][sl], 5.0)
+        assert np.array_equal(c[sl], co)
+        np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
+def test_mixed_one_image_and_general_tiles(ctx):
+    # FCC-256 (one-image count kernel + its hit masks) alternating with SC-64 (general search):
+    # the Betti search reads the masks of the one-image tiles only
+    batch = mixed_batch(2)
+    f, c = ctx.host_betti(batch, 5.0)
+    off = batch["atom_offset"]
+    for s in range(len(off) - 1):
+        sl = slice(off[s], off[s + 1])
         fo, co = O.structure_betti(batch["lattice"][s], batch["positions"][sl], batch["species"][sl], 5.0)
         assert np.array_equal(c[sl], co)
         np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)

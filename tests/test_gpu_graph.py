@@ -4,7 +4,7 @@ import os
 
 import numpy as np
 import pytest
-from conftest import GOLDEN
+from conftest import GOLDEN, mixed_batch
 
 import dgn
 import oracle_py as O
@@ -118,6 +118,19 @@ def test_empty_and_ragged(ctx, k, rbf_rc, dtype):
     ref = np.stack([O.gaussian_rbf(d, rbf_rc, 0.1) for d in dist])
     assert g["rbf"].shape == ref.shape
     np.testing.assert_allclose(g["rbf"], ref, rtol=1e-13 if dtype == dgn.DGN_F64 else RBF_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("npairs", [8, 520])
+def test_mixed_one_image_and_general_tiles(ctx, npairs):
+    # 8 pairs: 2,560 atoms, 4-atom count tiles; 520 pairs: 166,400 atoms, 64-atom tiles (some
+    # straddle an FCC and an SC cell)
+    batch = mixed_batch(npairs)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F64,
+                         write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, 5.0, 20)
+    assert np.array_equal(g["row_ptr"], rp) and np.array_equal(g["col"], col) and np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
 
 
 @pytest.mark.parametrize("layout", [0, 1])
