@@ -775,7 +775,7 @@ __device__ __forceinline__ int64_t mask_index(int64_t gi, int wd, int qa) {
 #define DGN_COUNT_WAVES 5
 #endif
 #ifndef DGN_COUNT1_WAVES
-#define DGN_COUNT1_WAVES 8
+#define DGN_COUNT1_WAVES 7
 #endif
 
 // the per-wave statistics of one tile, combined and stored with the tile's counts and masks
