@@ -1,6 +1,7 @@
 #!/bin/bash
-# round 3 A/B: waves-per-SIMD target of the fused emit (default = none: 88 VGPRs, 5 waves; 6; 7),
-# graph-only bench (f64 RBF headline configuration)
+# round 3 A/B: waves-per-SIMD target of the fused emit (default = none: 88 VGPRs, 5 waves; 6; 7), via a
+# temporary amdgpu_waves_per_eu(DGN_EMIT_WAVES) hook on graph_emit_kernel (not kept: no gain),
+# libdgn_e6/e7 built with tools/build_variant.sh; graph-only bench (f64 RBF headline configuration)
 set -eo pipefail
 OUT=gpurun_out/r03_ewaves
 mkdir -p "$OUT"
