@@ -192,3 +192,20 @@ def test_wide_in_kernel_overflow_retry(ctx):
     assert kt >= 1, kt
     kt = _check(ctx, clouds, npts, 2.0, 4096)  # natural caps again: no retry
     assert kt == 0, kt
+
+
+def test_above_1024_points_fails_loudly(ctx):
+    # outside the envelope: an explicit DGN_ERR_UNSUPPORTED, never a silent or
+    # truncated result -- a caller-given 1,100-point cloud, and FCC-256 at 15.5 A (≈ 1,300-point
+    # local complexes, the count pass finds them before any Betti launch)
+    rng = np.random.default_rng(5)
+    cloud = rng.uniform(0.0, 100.0, size=(1, 1100, 3))
+    with pytest.raises(dgn.DgnError) as e:
+        ctx.host_persistence(cloud, np.array([1100], np.int32), 1.0)
+    assert e.value.status == 5
+    with pytest.raises(dgn.DgnError) as e:
+        ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 15.5)
+    assert e.value.status == 5
+    # the context stays usable
+    f, c = ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 5.0)
+    assert (c >= 0).all()
