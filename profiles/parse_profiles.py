@@ -47,6 +47,20 @@ def main():
             summary["kernel_stats"] = {r["Name"]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                                                    "total_ns": float(r["TotalDurationNs"]),
                                                    "percent": float(r["Percentage"])} for r in csv.DictReader(f)}
+    # per-launch durations of the path kernels and the Betti kernels in dispatch order (the stats'
+    # averages mix the timed full-shard launches with the bench's warm-up, parity and f32 side
+    # launches; the bench's HIP-event averages cover the timed launches only)
+    trace = find(os.path.join(a.dir, "trace"), "*kernel_trace.csv")
+    if trace:
+        launches = {}
+        with open(trace) as f:
+            for r in csv.DictReader(f):
+                name = r["Kernel_Name"]
+                for k in PATH_KERNELS + ("betti_dist_search_kernel", "betti_kernel<44>", "betti_kernel<48>"):
+                    if k in name:
+                        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+                        launches.setdefault(k, []).append(round(ms, 4))
+        summary["trace_launch_ms"] = launches
     for name in ("trace_bench", "fetch_bench", "write_bench"):
         p = os.path.join(a.dir, f"{name}.json")
         if os.path.exists(p):
