@@ -47,6 +47,10 @@ constexpr int kChunk = DGN_CHUNK;  // complexes per dequeue (1: the grid drains 
 #define DGN_PV_UNROLL 4
 #endif
 constexpr int kPvUnroll = DGN_PV_UNROLL;  // V entries per step of the pivot search
+#ifndef DGN_APP_STEPS
+#define DGN_APP_STEPS 1
+#endif
+constexpr int kAppSteps = DGN_APP_STEPS;  // walk steps of an apparent pass's first round
 
 constexpr uint64_t kInf = ~0ull;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -88,7 +92,10 @@ struct ScratchLayout {
     static constexpr int64_t edges = (mincof_e + (64 * 63 / 2) + 15) / 16 * 16;  // uint16 [C(64,2)] (i << 8 | j)
     static constexpr int64_t tris = (edges + 2 * (64 * 63 / 2) + 15) / 16 * 16;  // uint32 [C(64,3)] packed triangles
     static constexpr int64_t d0 = tris + 4 * (64 * 63 * 62 / 6);    // f32 [64] dim-0 deaths
-    static constexpr int64_t total = d0 + 4 * 64;
+    // columns whose min-cofacet walk did not finish in the first round of an apparent pass (packed
+    // edge or triangle), walked to the end by a second round over this list
+    static constexpr int64_t defer = d0 + 4 * 64;                    // uint32 [C(64,3)]
+    static constexpr int64_t total = defer + 4 * (64 * 63 * 62 / 6);
 };
 
 // Per-wave LDS. The tiers are sized for resident waves: NP = 44 (the typical 5 A complex of
@@ -128,6 +135,11 @@ __device__ __forceinline__ uint32_t pin(uint32_t x) {
 __device__ __forceinline__ int pin(int x) {
     asm volatile("" : "+v"(x));
     return x;
+}
+// lanes [0, m) as a mask (m wave-uniform: scalar code). ballot(cmp) & lanes_below(m) keeps a
+// ballot to one v_cmp, where ballot(lane < m && cmp) materializes the combined bool first.
+__device__ __forceinline__ uint64_t lanes_below(int m) {
+    return m >= 64 ? ~0ull : (m <= 0 ? 0ull : (1ull << m) - 1ull);
 }
 __device__ __forceinline__ int c2(int x) { return x * (x - 1) / 2; }
 __device__ __forceinline__ int c3(int x) { return x * (x - 1) * (x - 2) / 6; }
@@ -210,9 +222,14 @@ struct Complex {
     mutable uint32_t walk_steps = 0;  // min-cofacet walk steps of this lane (lane efficiency)
     uint64_t* ph = nullptr;
     uint64_t* tprev = nullptr;
+    int sdim = 0;  // dimension of the serial walk in progress (DGN_DIAG_DIM: count only that one)
+#ifndef DGN_DIAG_DIM
+#define DGN_DIAG_DIM 0
+#endif
+    __device__ bool tagged() const { return DGN_DIAG_DIM == 0 || sdim == 0 || sdim == DGN_DIAG_DIM; }
     __device__ void stamp(int k) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
-        ph[k] += t - *tprev;
+        if (tagged()) ph[k] += t - *tprev;
         *tprev = t;
     }
 #define DGN_SUB(k) stamp(k)
@@ -272,8 +289,11 @@ struct Complex {
     // the simplex are all <= its diameter is the F-minimal cofacet and ends the search (found).
     // Only the winner's packed tuple is built. bk = the inserted vertex; when found, hda/hdb/hdc
     // are its distances to a, b, c, so the apparent test needs no further reads.
-    __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, uint32_t dbits, uint64_t cand, int& bk,
-                                         bool& found, uint32_t& hda, uint32_t& hdb, uint32_t& hdc) const {
+    // At most `steps` steps of four candidates are walked; `cand` returns the candidates not
+    // walked (nonzero with !found: the walk is unfinished and the result is not the minimum).
+    __device__ uint64_t min_cofacet_lane(int dim, int a, int b, int c, uint32_t dbits, uint64_t& cand, int& bk,
+                                         bool& found, uint32_t& hda, uint32_t& hdb, uint32_t& hdc,
+                                         int steps) const {
         uint32_t bd = 0xFFFFFFFFu;  // diameter of the best cofacet so far
         bk = -1;
         found = false;
@@ -282,7 +302,7 @@ struct Complex {
         const uint32_t* rb = Db() + b * S;
         const uint32_t* rcv = Db() + c * S;
         // four candidates per step (descending), their distance reads issued together
-        while (cand) {
+        for (int st = 0; cand && st < steps; ++st) {
 #ifdef DGN_PHASE_TIMING
             ++walk_steps;
 #endif
@@ -345,32 +365,8 @@ struct Complex {
     // cleared triangles hold kNone), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         const uint32_t f = uni(max_facet(dim, uni64(tau)));
-#ifdef DGN_APP_LDS
-        // f's F-minimal cofacet re-derived from the LDS matrix instead of the scratch table (one
-        // dependent global read less per owner lookup): lane k = candidate vertex k; the minimal
-        // diameter, then the largest k (the lane pass's walk). Tree edges and cleared triangles
-        // need no mark: such an f is already in a persistence pair (dim 0 / dim 1), so it is
-        // never in an apparent pair and the test below fails for it by itself.
-        const int k = lane_id();
-        const int a = dim == 1 ? (int)((f >> 8) & 255) : (int)((f >> 16) & 255);
-        const int b = dim == 1 ? (int)(f & 255) : (int)((f >> 8) & 255);
-        const int c = (int)(f & 255);
-        const uint32_t ds = dim == 1 ? dlowb(a, b) : tri_diamb(a, b, c);
-        uint32_t dd = max(Db()[a * S + k], Db()[b * S + k]);
-        if (dim == 2) dd = max(dd, Db()[c * S + k]);
-        // k is a common neighbour iff every distance is <= thr (the +inf diagonal excludes f's own
-        // vertices; lanes k >= n read past the rows and are not vertices)
-        const bool ok = k < n && dd <= __float_as_uint(thr);
-        const uint32_t key = ok ? max(dd, ds) : 0xFFFFFFFFu;
-        const uint32_t m = wave_min_u32(key);
-        const uint64_t bal = ballot(ok && key == m);
-        if (!bal) return kNone;
-        const uint32_t kb = (uint32_t)(63 - __clzll((long long)bal));
-        return kb == extra_vertex(key_packed(tau), f) ? f : kNone;
-#else
         const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
         return uni(m) == extra_vertex(key_packed(tau), f) ? f : kNone;
-#endif
     }
 
     __device__ uint64_t column_key(int dim, uint32_t cp) const {
@@ -384,10 +380,10 @@ struct Complex {
 
     __device__ int find_pivot(int npiv, uint64_t tau) const {
         const int lane = lane_id();
-        uint64_t bal = ballot(lane < npiv && pk0 == tau);
+        uint64_t bal = ballot(pk0 == tau) & lanes_below(npiv);
         if (bal) return __ffsll((unsigned long long)bal) - 1;
         if (npiv > kWave) {
-            bal = ballot(lane + kWave < npiv && pk1 == tau);
+            bal = ballot(pk1 == tau) & lanes_below(npiv - kWave);
             if (bal) return kWave + __ffsll((unsigned long long)bal) - 1;
         }
         const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
@@ -434,11 +430,10 @@ struct Complex {
         }
     }
     __device__ int v_find(uint32_t x, int v) const {
-        const int lane = lane_id();
-        uint64_t bal = ballot(lane < v && vs0 == x);
+        uint64_t bal = ballot(vs0 == x) & lanes_below(v);
         if (bal) return __ffsll((unsigned long long)bal) - 1;
         if (v > 64) {
-            bal = ballot(lane + 64 < v && vs1 == x);
+            bal = ballot(vs1 == x) & lanes_below(v - 64);
             if (bal) return 64 + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
@@ -467,39 +462,28 @@ struct Complex {
     // tau in V, always in a different lane (k = tau \ s), so the multiplicity of the wave
     // minimum is the popcount of a ballot. Even multiplicity: raise the floor and repeat.
     // kInf for the zero column.
-    // key of the cofacet s u {k} for lane k; its high word is 0xFFFFFFFF (above every real key)
-    // if k is not a common neighbour of s. Branch-free: every select is a v_cndmask.
-    __device__ uint64_t cofacet_key(int dim, int k, uint32_t sp_, uint32_t ds) const {
+    // key of the cofacet s u {k} for lane k (k < n); its high word is 0xFFFFFFFF (above every real
+    // key) if k is not a common neighbour of s: the LDS matrix holds all-ones for distances above
+    // thr and on the diagonal, so the diameter maximum carries it. The low word, ~packed(tau), is
+    // built in one v_perm_b32 from the complemented tuple of s (nsp = ~sp_) and lane k's
+    // complemented vertex byte (kc = 255 - k, perm byte 4), with the byte order picked by where k
+    // falls among the vertices of s (selector table kSel*). Branch-free: v_cndmask only.
+    __device__ uint64_t cofacet_key(int dim, int k, uint32_t kc, uint32_t sp_, uint32_t ds) const {
         const int a = dim == 1 ? (int)((sp_ >> 8) & 255) : (int)((sp_ >> 16) & 255);
         const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
         const int c = (int)(sp_ & 255);
-        // lane k reads row entries (x, k): consecutive lanes, consecutive banks. Lanes with
-        // k >= NP read past the matrix into adj/tree (still inside the struct) and are masked
-        // off by k < n. Every select arm is materialized (pin): v_cndmask, never exec branches.
+        // lane k reads row entries (x, k): consecutive lanes, consecutive banks
         uint32_t dd = max(ds, max(Db()[a * S + k], Db()[b * S + k]));
-        uint32_t pk;
-        const uint32_t uk = (uint32_t)k;
+        uint32_t sel;
         if (dim == 1) {
-            // insert k into (a > b): k > a -> (k,a,b); a > k > b -> (a,k,b); else (a,b,k)
-            const uint32_t ab = sp_ & 0xFFFFu;
-            const uint32_t p1 = pin((uk << 16) | ab);
-            const uint32_t p2 = pin(((uint32_t)a << 16) | (uk << 8) | (uint32_t)b);
-            const uint32_t p3 = pin((ab << 8) | uk);
-            pk = k > a ? p1 : (k > b ? p2 : p3);
+            // ~(k,a,b) / ~(a,k,b) / ~(a,b,k); the top byte of ~pack3 is 0xFF (S1 byte 2 of ~sp_)
+            sel = k > a ? 0x02040100u : (k > b ? 0x02010400u : 0x02010004u);
         } else {
             dd = max(dd, Db()[c * S + k]);
-            const uint32_t abc = sp_ & 0xFFFFFFu;
-            const uint32_t p1 = pin((uk << 24) | abc);
-            const uint32_t p2 = pin(((uint32_t)a << 24) | (uk << 16) | (abc & 0xFFFFu));
-            const uint32_t p3 = pin(((abc >> 8) << 16) | (uk << 8) | (uint32_t)c);
-            const uint32_t p4 = pin((abc << 8) | uk);
-            pk = k > a ? p1 : (k > b ? p2 : (k > c ? p3 : p4));
+            sel = k > a ? 0x04020100u : (k > b ? 0x02040100u : (k > c ? 0x02010400u : 0x02010004u));
         }
-        // k is a common neighbour iff every distance to it is <= thr (sparse_distance_matrix):
-        // the diameter bound covers it, the +inf diagonal excludes k in the simplex, and lanes
-        // k >= n (reading past the row) are not vertices
-        dd = (k < n && dd <= __float_as_uint(thr)) ? dd : 0xFFFFFFFFu;
-        return ((uint64_t)dd << 32) | (uint64_t)(~pk);
+        const uint32_t nk = __builtin_amdgcn_perm(kc, ~sp_, sel);
+        return ((uint64_t)dd << 32) | (uint64_t)nk;
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
@@ -511,6 +495,7 @@ struct Complex {
     // kInf for the zero column.
     __device__ uint64_t pivot_of_V(int dim, int v_, uint64_t floor) {
         const int k = lane_id();
+        const uint32_t kc = 255u - (uint32_t)k;
         const int v = (int)uni((uint32_t)v_);
         if (k < v) vd0 = simplex_diam(dim, vs0);
         if (v > 64 && k + 64 < v) vd1 = simplex_diam(dim, vs1);
@@ -529,22 +514,24 @@ struct Complex {
                 for (; i + kPvUnroll <= cnt; i += kPvUnroll) {
                     uint64_t kq[kPvUnroll];
 #pragma unroll
-                    for (int u = 0; u < kPvUnroll; ++u) kq[u] = cofacet_key(dim, k, rl(vs, i + u), rl(vdb, i + u)) - base;
+                    for (int u = 0; u < kPvUnroll; ++u) kq[u] = cofacet_key(dim, k, kc, rl(vs, i + u), rl(vdb, i + u)) - base;
 #pragma unroll
                     for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
                 }
                 for (; i < cnt; ++i) {
-                    const uint64_t key = cofacet_key(dim, k, rl(vs, i), rl(vdb, i)) - base;
+                    const uint64_t key = cofacet_key(dim, k, kc, rl(vs, i), rl(vdb, i)) - base;
                     lmin = key < lmin ? key : lmin;
                 }
             };
-            scan(vs0, __float_as_uint(vd0), v < 64 ? v : 64);
-            if (v > 64) scan(vs1, __float_as_uint(vd1), v - 64);
+            // lanes k >= n are not vertices: they keep kInf (exec-masked, no per-entry test)
+            if (k < n) {
+                scan(vs0, __float_as_uint(vd0), v < 64 ? v : 64);
+                if (v > 64) scan(vs1, __float_as_uint(vd1), v - 64);
+            }
             const uint64_t mt = wave_min_u64(lmin);
             const uint64_t m = mt + base;
 #ifdef DGN_PHASE_TIMING
-            ph[24] += 1;
-            ph[25] += (uint64_t)v;
+            if (tagged()) { ph[24] += 1; ph[25] += (uint64_t)v; }
 #endif
             // no cofacet above floor: the minimum is a non-neighbour key (high word all ones) or
             // a wrapped key <= floor
@@ -568,6 +555,9 @@ struct Complex {
     // initial pivot, all computed lane-parallel; larger sets are rank-sorted into scratch.
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
+#ifdef DGN_PHASE_TIMING
+        sdim = dim;
+#endif
         if (nna > kNACap) { err |= kErrNA; return; }
         const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
         const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
@@ -643,7 +633,7 @@ struct Complex {
             DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
 #ifdef DGN_PHASE_TIMING
-            ph[27] += (owner < 0 && app == kNone) ? 1 : 0;  // settled by its initial pivot
+            if (tagged()) ph[27] += (owner < 0 && app == kNone) ? 1 : 0;  // settled by its initial pivot
 #endif
             if (owner >= 0 || app != kNone) {
                 v_toggle(dim, cp, v);
@@ -681,9 +671,11 @@ struct Complex {
                     ++n_adds;
                     DGN_SUB(20);
 #ifdef DGN_PHASE_TIMING
-                    ph[14] += (uint64_t)v;
-                    ph[15] += (uint64_t)v * (uint64_t)v;
-                    ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
+                    if (tagged()) {
+                        ph[14] += (uint64_t)v;
+                        ph[15] += (uint64_t)v * (uint64_t)v;
+                        ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
+                    }
 #endif
                     tau = v > 0 ? pivot_of_V(dim, v, tau) : kInf;
                     DGN_SUB(21);
@@ -696,7 +688,7 @@ struct Complex {
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
 #ifdef DGN_PHASE_TIMING
-                ph[28] += tau == kInf ? 1 : 0;
+                if (tagged()) ph[28] += tau == kInf ? 1 : 0;
 #endif
                 if (tau == kInf) continue;  // zero column
             }
@@ -747,6 +739,13 @@ struct Complex {
     do {             \
     } while (0)
 #endif
+// VALU accounting builds only (-DDGN_STOP_AT=k): leave the complex after phase k
+#ifdef DGN_STOP_AT
+#define DGN_STOP(k) \
+    if (DGN_STOP_AT == (k)) { lds_sync(); continue; }
+#else
+#define DGN_STOP(k)
+#endif
 
 template <int NP>
 __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kernel(BettiLaunch bl) {
@@ -763,8 +762,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
     const int lane = lane_id();
-    // +inf diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key)
-    if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0x7F800000u);
+    // all-ones diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key)
+    if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0xFFFFFFFFu);
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;
 
@@ -838,64 +837,80 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         i -= c2(i) > t;
                         i += c2(i + 1) <= t;
                         const int j = t - c2(i);
+                        // distances above thr are never read as lengths (every simplex of the
+                        // complex has edges <= thr): stored as all-ones, so a cofacet through a
+                        // non-neighbour gets an all-ones diameter by the maximum alone
+                        const float w = v[u] <= cx.thr ? v[u] : __uint_as_float(0xFFFFFFFFu);
                         if (t < tot) {
-                            s.D[i * S + j] = v[u];
-                            s.D[j * S + i] = v[u];
+                            s.D[i * S + j] = w;
+                            s.D[j * S + i] = w;
                         }
                     }
                 }
             }
             lds_sync();
-            DGN_PHASE(0);
+            DGN_PHASE(0); DGN_STOP(1)
             // ---- adjacency (sparse_distance_matrix: i != j and d <= thr, ripser.cpp:386-395) ----
+            uint64_t myadj = 0;  // this lane's row
             {
-                uint64_t m = 0;
                 for (int i = 0; i < n; ++i) {
-                    const uint64_t row = ballot(lane < n && lane != i && s.D[i * S + lane] <= cx.thr);
-                    if (lane == i) m = row;
+                    // the all-ones diagonal (NaN) fails the test: no self loops
+                    const uint64_t row = ballot(s.D[i * S + lane] <= cx.thr) & lanes_below(n);
+                    myadj = lane == i ? row : myadj;
                 }
-                s.adj[lane] = lane < n ? m : 0ull;
-                if (lane < NP) s.par[lane] = 0xFF;
+                if (lane < NP) s.adj[lane] = myadj;  // (lanes >= NP would write past adj)
             }
-            lds_sync();
             float* d0s = cx.template sp<float>(ScratchLayout::d0);
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
             cx.n_d0 = 0;
             // ---- dim 0: Prim on F-keys == Kruskal's forest in Ripser order (ripser.cpp:725-762) ----
+            // best = the lane's F-minimal edge to the forest (kInf once the lane is in the forest,
+            // and for lanes >= n); the wave minimum of its high word (the diameter) alone decides
+            // unless two lanes tie on it. Deaths and forest parents stay in registers (lane t: death
+            // t; each lane its own parent) and are written once after the loop.
             {
-                bool in_tree = lane == 0;
+                bool in_tree = lane == 0, root = lane == 0;
                 int parent = 0;
+                float death = 0.f;
                 uint64_t best = kInf;
-                if (lane < n && lane != 0 && ((s.adj[0] >> lane) & 1ull)) best = cx.ekey(0, lane);
+                if (lane < n && lane != 0 && (myadj & 1ull)) best = cx.ekey(0, lane);
                 if (n >= 1) cx.n_inf0 = 1;
-                int added = 1;
-                while (added < n) {
-                    const uint64_t cand = (lane < n && !in_tree) ? best : kInf;
-                    const uint64_t kmin = wave_min_u64(cand);
+                uint64_t tree = 1;  // forest vertices (uniform)
+                for (int added = 1; added < n; ++added) {
+                    const uint32_t hi = (uint32_t)(best >> 32);
+                    const uint32_t mh = wave_min_u32(hi);
                     int v;
-                    if (kmin == kInf) {  // new component: lowest vertex outside the forest
-                        const uint64_t out = ballot(lane < n && !in_tree);
-                        v = __ffsll((unsigned long long)out) - 1;
+                    bool newcomp = false;
+                    if (mh == 0xFFFFFFFFu) {  // new component: lowest vertex outside the forest
+                        v = __ffsll((unsigned long long)(~tree & lanes_below(n))) - 1;
                         cx.n_inf0 += 1;
+                        newcomp = true;
                     } else {
-                        const uint64_t bal = ballot(cand == kmin);
+                        uint64_t bal = ballot(hi == mh);
+                        if (__popcll(bal) > 1) {  // equal diameters: the low words (F-order index) decide
+                            const uint32_t ml = wave_min_u32(hi == mh ? (uint32_t)best : 0xFFFFFFFFu);
+                            bal = ballot(best == (((uint64_t)mh << 32) | ml));
+                        }
                         v = __ffsll((unsigned long long)bal) - 1;
-                        const int u = __shfl(parent, v, kWave);
-                        const float dd = key_diam(kmin);
-                        if (dd != 0.0f) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
-                            if (lane == 0) d0s[cx.n_d0] = dd;
+                        if (__uint_as_float(mh) != 0.0f) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
+                            death = lane == cx.n_d0 ? __uint_as_float(mh) : death;
                             cx.n_d0 += 1;
                         }
-                        if (lane == 0) s.par[v] = (uint8_t)u;
                     }
-                    if (lane == v) in_tree = true;
-                    ++added;
-                    if (lane < n && !in_tree && ((s.adj[v] >> lane) & 1ull)) {
+                    tree |= 1ull << v;
+                    if (lane == v) {
+                        in_tree = true;
+                        root = newcomp;
+                        best = kInf;
+                    }
+                    if (!in_tree && ((myadj >> v) & 1ull)) {
                         const uint64_t k = cx.ekey(v, lane);
                         if (k < best) { best = k; parent = v; }
                     }
                 }
+                if (lane < cx.n_d0) d0s[lane] = death;
+                if (lane < NP) s.par[lane] = (lane < n && !root) ? (uint8_t)parent : (uint8_t)0xFF;
             }
             lds_sync();
             // ---- edge list (i > j, d <= thr), row-major ----
@@ -917,51 +932,52 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             __syncthreads();  // edge list (global scratch) visible to every lane
             cx.n_p1 = 0;
             cx.n_p2 = 0;
-            DGN_PHASE(1);
+            DGN_PHASE(1); DGN_STOP(2)
             uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
             uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
             uint8_t* mincof = cx.template sp<uint8_t>(ScratchLayout::mincof);
             uint8_t* mincof_e = cx.template sp<uint8_t>(ScratchLayout::mincof_e);
                     // ---- dim 1: one lane per column (non-tree edge) ----
+            uint32_t* defer = cx.template sp<uint32_t>(ScratchLayout::defer);
             if (dim_max >= 1) {
-                int nna = 0;
-                for (int base = 0; base < n_edges; base += kWave) {
-                    const int e = base + lane;
-                    bool apparent = false, na_col = false;
-                    float birth = 0.f, death = 0.f;
+                int nna = 0, ndef = 0;
+                // One lane per edge column. Round A walks at most kAppSteps steps of every column's
+                // min-cofacet walk; columns not settled by then are listed and walked to the end by
+                // round B, so a round-synchronous pass is not paced by its few long walks.
+                auto edge_col = [&](bool active, uint32_t ed, int steps) {
+                    bool na_col = false, dfr = false;
                     uint64_t colkey = 0, best = kInf;
-                    if (e < n_edges) {
-                        const uint32_t ed = edges[e];
+                    if (active) {
                         const int i = ed >> 8, j = ed & 255;
                         uint32_t mc = kMcNone;
                         if (!cx.is_tree(i, j)) {
-                            birth = cx.dlow(i, j);
+                            const float birth = cx.dlow(i, j);
                             colkey = make_key(birth, pack2(i, j));
-                            const uint64_t cand = s.adj[i] & s.adj[j];
+                            uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
                                 const uint32_t dij = __float_as_uint(birth);
                                 int bk;
                                 bool found;
                                 uint32_t hda, hdb, hdc;
-                                best = cx.min_cofacet_lane(1, i, j, 0, dij, cand, bk, found, hda, hdb, hdc);
-                                death = key_diam(best);
+                                best = cx.min_cofacet_lane(1, i, j, 0, dij, cand, bk, found, hda, hdb, hdc, steps);
+                                dfr = !found && cand != 0;
                                 // apparent iff (i,j) is the F-max facet of its pivot triangle: a
                                 // zero-persistence cofacet whose other facets (bk replacing i or j)
                                 // are shorter, or as long with a larger index (bk above the
-                                // replaced vertex)
-                                apparent = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
+                                // replaced vertex). An apparent pair has zero persistence: no pair
+                                // is emitted (death > birth only, ripser.cpp:1240).
+                                const bool apparent = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
                                 if (apparent) {
                                     const uint32_t tp = key_packed(best);
                                     cx.set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
                                 } else {
-                                    na_col = true;
+                                    na_col = !dfr;
                                 }
                                 mc = (uint32_t)bk;
                             }
                         }
-                        mincof_e[edge_dense(i, j)] = (uint8_t)mc;
+                        if (!dfr) mincof_e[edge_dense(i, j)] = (uint8_t)mc;
                     }
-                    cx.append_pairs(1, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
@@ -971,16 +987,31 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         }
                     }
                     nna += __popcll(bal);
+                    const uint64_t bd = ballot(dfr);
+                    if (dfr) defer[ndef + mask_prefix(bd)] = ed;
+                    ndef += __popcll(bd);
+                };
+                for (int base = 0; base < n_edges; base += kWave) {
+                    const int e = base + lane;
+                    edge_col(e < n_edges, e < n_edges ? (uint32_t)edges[e] : 0u, kAppSteps);
+                }
+                if (ndef) {
+                    __syncthreads();  // the deferred list (scratch) is read by other lanes
+                    const int nd = ndef;
+                    for (int base = 0; base < nd; base += kWave) {
+                        const int e = base + lane;
+                        edge_col(e < nd, e < nd ? defer[e] : 0u, 1 << 20);
+                    }
                 }
                 __syncthreads();
-                DGN_PHASE(2);
+                DGN_PHASE(2); DGN_STOP(3)
 #ifdef DGN_PHASE_TIMING
                 ph[8] += nna;
                 const int a0 = cx.n_adds;
 #endif
                 cx.reduce_serial(1, nna);
                 __syncthreads();  // clearing marks (scratch stores) complete before the dim-2 pass
-                DGN_PHASE(3);
+                DGN_PHASE(3); DGN_STOP(4)
 #ifdef DGN_PHASE_TIMING
                 ph[10] += cx.n_adds - a0;
 #endif
@@ -1044,23 +1075,15 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     }
                 }
                 __syncthreads();  // the list (scratch) is read by other lanes
-                DGN_PHASE(26);
-                // (2b) one lane per column (uncleared triangle). Global reads leave the per-round
-                // dependency chain: list entries are fetched two rounds ahead, their clearing
-                // bytes one round ahead.
-                uint32_t tp1 = lane < ntri ? tl[lane] : 0u;
-                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
-                uint32_t tp2 = kWave + lane < ntri ? tl[kWave + lane] : 0u;
-                for (int base = 0; base < ntri; base += kWave) {
-                    const uint32_t tp = tp1, clb = cl1;
-                    const bool active = base + lane < ntri;
-                    tp1 = tp2;
-                    cl1 = base + kWave + lane < ntri
-                              ? (uint32_t)mincof[tri_dense((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
-                              : 0u;
-                    tp2 = base + 2 * kWave + lane < ntri ? tl[base + 2 * kWave + lane] : 0u;
-                    bool apparent = false, na_col = false;
-                    float birth = 0.f, death = 0.f;
+                DGN_PHASE(26); DGN_STOP(5)
+                // (2b) one lane per column (uncleared triangle), in two rounds as in the dim-1
+                // pass: round A walks at most kAppSteps steps per column and lists the unsettled
+                // ones, round B walks those to the end. Global reads leave the per-round dependency
+                // chain: list entries are fetched two rounds ahead, their clearing bytes one round
+                // ahead.
+                int ndef = 0;
+                auto tri_col = [&](bool active, uint32_t tp, uint32_t clb, int steps) {
+                    bool na_col = false, dfr = false;
                     uint64_t colkey = 0, best = kInf;
                     if (active) {
                         const int a = (tp >> 16) & 255, b = (tp >> 8) & 255, c = tp & 255;
@@ -1068,25 +1091,25 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         if (clb != kMcCleared) {
                             const uint32_t dab = cx.dlowb(a, b), dac = cx.dlowb(a, c), dbc = cx.dlowb(b, c);
                             const uint32_t ds = max(max(dab, dac), dbc);
-                            birth = __uint_as_float(ds);
-                            colkey = make_key(birth, tp);
-                            const uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
+                            colkey = make_key(__uint_as_float(ds), tp);
+                            uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
                             if (cand) {
                                 int bk;
                                 bool found;
                                 uint32_t hda, hdb, hdc;
-                                best = cx.min_cofacet_lane(2, a, b, c, ds, cand, bk, found, hda, hdb, hdc);
-                                death = key_diam(best);
+                                best = cx.min_cofacet_lane(2, a, b, c, ds, cand, bk, found, hda, hdb, hdc, steps);
+                                dfr = !found && cand != 0;
                                 // apparent iff (a,b,c) is the F-max facet of its pivot tetrahedron
-                                // (the dim-1 facet test, one facet per replaced vertex)
-                                apparent = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
-                                           (bk > b || max(max(hda, hdc), dac) < ds) &&
-                                           (bk > c || max(max(hda, hdb), dab) < ds);
-                                na_col = !apparent;
+                                // (the dim-1 facet test, one facet per replaced vertex); zero
+                                // persistence, so no pair is emitted
+                                const bool apparent = found && (bk > a || max(max(hdb, hdc), dbc) < ds) &&
+                                                      (bk > b || max(max(hda, hdc), dac) < ds) &&
+                                                      (bk > c || max(max(hda, hdb), dab) < ds);
+                                na_col = !apparent && !dfr;
                                 mc = (uint32_t)bk;
                             }
                         }
-                        mincof[tri_dense(a, b, c)] = (uint8_t)mc;
+                        if (!dfr) mincof[tri_dense(a, b, c)] = (uint8_t)mc;
                     }
 #ifdef DGN_PHASE_TIMING
                     // lane efficiency of the round-synchronous walk: steps summed over lanes [29],
@@ -1102,7 +1125,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         }
                     }
 #endif
-                    cx.append_pairs(2, apparent && death > birth, birth, death);
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
@@ -1112,9 +1134,35 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         }
                     }
                     nna += __popcll(bal);
+                    const uint64_t bd = ballot(dfr);
+                    if (dfr) defer[ndef + mask_prefix(bd)] = tp;
+                    ndef += __popcll(bd);
+                };
+                uint32_t tp1 = lane < ntri ? tl[lane] : 0u;
+                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
+                uint32_t tp2 = kWave + lane < ntri ? tl[kWave + lane] : 0u;
+                for (int base = 0; base < ntri; base += kWave) {
+                    const uint32_t tp = tp1, clb = cl1;
+                    const bool active = base + lane < ntri;
+                    tp1 = tp2;
+                    cl1 = base + kWave + lane < ntri
+                              ? (uint32_t)mincof[tri_dense((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
+                              : 0u;
+                    tp2 = base + 2 * kWave + lane < ntri ? tl[base + 2 * kWave + lane] : 0u;
+                    tri_col(active, tp, clb, kAppSteps);
+                }
+                if (ndef) {
+                    __syncthreads();  // the deferred list (scratch) is read by other lanes
+                    const int nd = ndef;
+                    uint32_t tq = lane < nd ? defer[lane] : 0u;
+                    for (int base = 0; base < nd; base += kWave) {
+                        const uint32_t tp = tq;
+                        tq = base + kWave + lane < nd ? defer[base + kWave + lane] : 0u;
+                        tri_col(base + lane < nd, tp, 0u, 1 << 20);  // deferred columns are never cleared
+                    }
                 }
                 __syncthreads();
-                DGN_PHASE(4);
+                DGN_PHASE(4); DGN_STOP(6)
 #ifdef DGN_PHASE_TIMING
                 ph[9] += nna;
                 const int a0 = cx.n_adds;

@@ -1,6 +1,7 @@
 """Generate the committed golden fixtures (run ONLY in the survey/build container).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # everything
+    python tests/golden/make_golden.py rc10     # only the 10 A fixtures (rc10.npz)
 
 Inputs: the reference's own POSCAR files (/root/reference/web/public/data/structures/*.vasp,
 parsed here as data) and synthetic SC cells from the bit-reproducible generator.
@@ -54,8 +55,31 @@ def betti_ref(lat, pos, species, rc):
     return f, c
 
 
+def rc10_fixtures():
+    """(iv) The reference's default Betti cutoff, r_cutoff = 10 (preprocess_betti.cpp:117): verbatim
+    Ripser counts and 35 statistics for EVERY atom of 741.vasp (N = 120) and of FCC-256 structure 0
+    of the synthetic generator (the bench workload; ~340-point complexes). The restated reduction
+    is not re-run here (minutes per structure single-threaded); the GPU tests compare against these
+    arrays directly. Written to rc10.npz."""
+    out = {}
+    lat, pos, sp = parse_poscar(os.path.join(REF_POSCARS, "741.vasp"))
+    f, c = O.ref_structure_betti(lat, pos, sp, 10.0, omp_threads=8, ripser_threads=1)
+    out["741/features"], out["741/counts"] = f, c
+    print("rc10 741", pos.shape[0], "atoms")
+    bt = synth.make_batch("fcc", 4, 1)
+    f, c = O.ref_structure_betti(bt["lattice"][0], bt["positions"], bt["species"], 10.0, omp_threads=8,
+                                 ripser_threads=1)
+    out["fcc256_0/features"], out["fcc256_0/counts"] = f, c
+    out["fcc256_0/positions"] = bt["positions"]  # the generator's output, for a bit-identity check
+    print("rc10 fcc256", bt["positions"].shape[0], "atoms")
+    np.savez_compressed(os.path.join(OUT, "rc10.npz"), **out)
+
+
 def main():
     assert O.ref_available(), "build oracle/_ref first (make -C oracle)"
+    if sys.argv[1:] == ["rc10"]:
+        rc10_fixtures()
+        return
     # (i) POSCARs: inputs + CSR at rc=5, K=12/20, RBF (rc=5, dr=0.1) of 1 / 741, Betti at rc=5 of all
     poscar = {}
     for path in sorted(glob.glob(os.path.join(REF_POSCARS, "*.vasp"))):
@@ -136,6 +160,7 @@ def main():
             kat[f"{name}/{d}"] = pr[d]
         kat[f"{name}/n_inf0"] = np.int32(pr["n_inf0"])
     np.savez_compressed(os.path.join(OUT, "kat.npz"), **kat)
+    rc10_fixtures()
     for f in sorted(glob.glob(os.path.join(OUT, "*.npz"))):
         print(f, os.path.getsize(f), "bytes")
 

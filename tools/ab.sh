@@ -1,0 +1,16 @@
+#!/bin/bash
+# A/B of libdgn builds on one GPU box, interleaved (tag1 tag2 ... tag1 tag2 ...):
+#   gpurun -- bash tools/ab.sh <outdir> <rounds> <tag>...   (tag "base" = libdgn.so, else libdgn_<tag>.so)
+# Each arm: the graph + Betti bench (3 steps, no CPU baseline, no side lines); prints value and betti_vr ms.
+set -eo pipefail
+OUT=$1; R=$2; shift 2
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for r in $(seq 1 $R); do
+  for tag in "$@"; do
+    lib=defect-gnn-cpp_amd/lib/libdgn.so; [ "$tag" != base ] && lib=defect-gnn-cpp_amd/lib/libdgn_$tag.so
+    DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-alt-rbf \
+        > "$OUT/${tag}_$r.json" 2>> "$OUT/err.log"
+    python3 -c "import json; r=json.load(open('$OUT/${tag}_$r.json')); k=r['kernel_ms_per_step']; print('$tag', r['value'], k.get('betti_vr'), k.get('betti_dist'), k.get('graph_emit'))"
+  done
+done
