@@ -110,8 +110,11 @@ struct BettiSmem {
     uint64_t adj[NP];
     uint8_t par[NP];                  // minimum spanning forest: parent of each vertex (0xFF = root)
 };
+#ifndef DGN_WAVES44
+#define DGN_WAVES44 5
+#endif
 template <int NP>
-constexpr int betti_waves_per_simd() { return NP <= 44 ? 5 : (NP <= 48 ? 4 : 3); }
+constexpr int betti_waves_per_simd() { return NP <= 44 ? DGN_WAVES44 : (NP <= 48 ? 4 : 3); }
 
 // ---------------------------------------------------------------------------------------
 // small helpers
@@ -301,8 +304,11 @@ struct Complex {
         const uint32_t* ra = Db() + a * S;  // rows a, b, c: entry k is d(., k)
         const uint32_t* rb = Db() + b * S;
         const uint32_t* rcv = Db() + c * S;
+        // the candidates bit-reversed: the largest remaining k is the lowest set bit, taken with a
+        // trailing-zero count and cleared with r & (r - 1) (no validity select: 0 stays 0)
+        uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)cand) << 32) | __builtin_bitreverse32((uint32_t)(cand >> 32));
         // four candidates per step (descending), their distance reads issued together
-        for (int st = 0; cand && st < steps; ++st) {
+        for (int st = 0; r && st < steps; ++st) {
 #ifdef DGN_PHASE_TIMING
             ++walk_steps;
 #endif
@@ -310,9 +316,9 @@ struct Complex {
             bool val[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                val[j] = cand != 0;
-                kk[j] = val[j] ? 63 - __clzll((long long)cand) : 0;
-                cand &= val[j] ? ~(1ull << kk[j]) : ~0ull;
+                val[j] = r != 0;
+                kk[j] = 63 - (val[j] ? __builtin_ctzll(r) : 63);
+                r &= r - 1;
             }
             uint32_t da[4], dbb[4], dc[4];
 #pragma unroll
@@ -335,6 +341,7 @@ struct Complex {
             }
             if (found) break;
         }
+        cand = r;  // nonzero: candidates left unwalked (only their count matters to the callers)
         if (bk < 0) return kInf;
         const uint32_t pk = dim == 1 ? tri_with(a, b, bk) : tet_with(a, b, c, bk);
         return ((uint64_t)bd << 32) | (uint64_t)(~pk);
@@ -528,7 +535,21 @@ struct Complex {
                 scan(vs0, __float_as_uint(vd0), v < 64 ? v : 64);
                 if (v > 64) scan(vs1, __float_as_uint(vd1), v - 64);
             }
-            const uint64_t mt = wave_min_u64(lmin);
+            // wave minimum: the high words first; a unique minimal high word settles it (and its
+            // multiplicity, 1) without the low-word stage
+            const uint32_t lhi = (uint32_t)(lmin >> 32);
+            const uint32_t mh = wave_min_u32(lhi);
+            const uint64_t bh = ballot(lhi == mh);
+            uint64_t mt;
+            int mult;
+            if (__popcll(bh) == 1) {
+                mt = ((uint64_t)mh << 32) | rl((uint32_t)lmin, __ffsll((unsigned long long)bh) - 1);
+                mult = 1;
+            } else {
+                const uint32_t ml = wave_min_u32(lhi == mh ? (uint32_t)lmin : 0xFFFFFFFFu);
+                mt = ((uint64_t)mh << 32) | ml;
+                mult = __popcll(ballot(lmin == mt));
+            }
             const uint64_t m = mt + base;
 #ifdef DGN_PHASE_TIMING
             if (tagged()) { ph[24] += 1; ph[25] += (uint64_t)v; }
@@ -536,7 +557,7 @@ struct Complex {
             // no cofacet above floor: the minimum is a non-neighbour key (high word all ones) or
             // a wrapped key <= floor
             if ((uint32_t)(m >> 32) == 0xFFFFFFFFu || m <= floor) return kInf;
-            if (__popcll(ballot(lmin == mt)) & 1) return m;
+            if (mult & 1) return m;
             floor = m;
         }
     }
