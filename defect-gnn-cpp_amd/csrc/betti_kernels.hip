@@ -158,9 +158,10 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xf, 0xf, false));
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xf, 0xf, false));
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xf, 0xf, false));
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
-    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), d = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
-    return min(min(a, b), min(c, d));
+    // row minima -> lane 63 by row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3): one readlane
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x142, 0xa, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     const uint32_t hi = (uint32_t)(v >> 32);
@@ -196,6 +197,12 @@ __device__ __forceinline__ uint32_t byte_sum(uint32_t p) { return (p & 255) + ((
 __device__ __forceinline__ uint32_t extra_vertex(uint32_t tau, uint32_t f) { return byte_sum(tau) - byte_sum(f); }
 __device__ __forceinline__ int tri_dense(int a, int b, int c) {  // combinatorial index, a > b > c
     return a * (a - 1) * (a - 2) / 6 + b * (b - 1) / 2 + c;
+}
+// per-lane form (vector registers): 24-bit multiplies and an exact f32 division by 6 (the
+// product is a multiple of 6 below 2^18) instead of a quarter-rate 32-bit multiply-high
+__device__ __forceinline__ int tri_dense_lane(int a, int b, int c) {
+    const uint32_t p = __umul24(__umul24((uint32_t)a, (uint32_t)(a - 1)), (uint32_t)(a - 2));
+    return (int)((float)p * (1.0f / 6.0f) + 0.5f) + (int)(__umul24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + c;
 }
 __device__ __forceinline__ int edge_dense(int a, int b) { return a * (a - 1) / 2 + b; }  // a > b
 // dense combinatorial index of a packed column simplex (edge for dim 1, triangle for dim 2)
@@ -267,6 +274,9 @@ struct Complex {
         return sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] == kMcCleared;
     }
     __device__ void set_cleared(int a, int b, int c) { sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] = kMcCleared; }
+    __device__ void set_cleared_lane(int a, int b, int c) {
+        sp<uint8_t>(ScratchLayout::mincof)[tri_dense_lane(a, b, c)] = kMcCleared;
+    }
     __device__ uint8_t* mincof_of(int dim) const {
         return sp<uint8_t>(dim == 1 ? ScratchLayout::mincof_e : ScratchLayout::mincof);
     }
@@ -990,7 +1000,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                                 const bool apparent = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
                                 if (apparent) {
                                     const uint32_t tp = key_packed(best);
-                                    cx.set_cleared((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
+                                    cx.set_cleared_lane((tp >> 16) & 255, (tp >> 8) & 255, tp & 255);
                                 } else {
                                     na_col = !dfr;
                                 }
@@ -1130,7 +1140,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                                 mc = (uint32_t)bk;
                             }
                         }
-                        if (!dfr) mincof[tri_dense(a, b, c)] = (uint8_t)mc;
+                        if (!dfr) mincof[tri_dense_lane(a, b, c)] = (uint8_t)mc;
                     }
 #ifdef DGN_PHASE_TIMING
                     // lane efficiency of the round-synchronous walk: steps summed over lanes [29],
@@ -1160,14 +1170,14 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     ndef += __popcll(bd);
                 };
                 uint32_t tp1 = lane < ntri ? tl[lane] : 0u;
-                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
+                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense_lane((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
                 uint32_t tp2 = kWave + lane < ntri ? tl[kWave + lane] : 0u;
                 for (int base = 0; base < ntri; base += kWave) {
                     const uint32_t tp = tp1, clb = cl1;
                     const bool active = base + lane < ntri;
                     tp1 = tp2;
                     cl1 = base + kWave + lane < ntri
-                              ? (uint32_t)mincof[tri_dense((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
+                              ? (uint32_t)mincof[tri_dense_lane((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
                               : 0u;
                     tp2 = base + 2 * kWave + lane < ntri ? tl[base + 2 * kWave + lane] : 0u;
                     tri_col(active, tp, clb, kAppSteps);
@@ -1179,7 +1189,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     for (int base = 0; base < nd; base += kWave) {
                         const uint32_t tp = tq;
                         tq = base + kWave + lane < nd ? defer[base + kWave + lane] : 0u;
-                        tri_col(base + lane < nd, tp, 0u, 1 << 20);  // deferred columns are never cleared
+                        // deferred columns are never cleared
+                        tri_col(base + lane < nd, tp, 0u, 1 << 20);
                     }
                 }
                 __syncthreads();

@@ -1,9 +1,13 @@
 """Wide local complexes (65..512 points: the reference's default 10 A cutoff) through the C ABI
 vs the reference's verbatim vendored Ripser (oracle/_ref) — counts and pairs bit-exact, the 35
-statistics within 1e-6 relative. Ripser takes ~1 s per 340-point complex on one core, so the
-10 A checks spot-check a few atoms."""
+statistics within 1e-6 relative. Every atom of 741.vasp and of one FCC-256 structure at 10 A is
+checked against committed verbatim-Ripser fixtures (tests/golden/rc10.npz, made by
+tests/golden/make_golden.py rc10); other 10 A checks spot-check atoms live (~1 s per complex)."""
+import os
+
 import numpy as np
 import pytest
+from conftest import GOLDEN
 
 import dgn
 import oracle_py as O
@@ -16,7 +20,7 @@ def _ref(low, n, thr):
     return O.ref_persistence(low, n, thr) if O.ref_available() else O.persistence(low, n, thr)
 
 
-WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG
+WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG (0: one wave per complex)
 
 
 def _check_clouds(ctx, clouds, npts, thr, cap):
@@ -58,27 +62,37 @@ def test_all_three_tiers_in_one_batch(ctx):
     _check_clouds(ctx, clouds, npts, 1.8, 4096)
 
 
-@pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
+def _rc10_inputs(name):
+    if name == "741":
+        fx = np.load(os.path.join(GOLDEN, "poscar_rc5.npz"))
+        pos = fx["741/positions"]
+        return {"lattice": fx["741/lattice"][None].copy(), "positions": pos.copy(),
+                "species": fx["741/species"].astype(np.int32), "atom_offset": np.array([0, len(pos)], np.int64)}
+    return dgn.synth_batch("fcc", 4, 1)
+
+
 @pytest.mark.parametrize("wg", [0, 1])
-def test_fcc256_default_cutoff_10A(ctx, wg):
-    """compute_structure_betti_features at the reference default r_cutoff = 10 (~340-point
-    complexes), with the one-wave and the workgroup-per-complex wide kernels; spot-check atoms
-    against the verbatim Ripser, and the two kernels against each other on every atom."""
-    batch = dgn.synth_batch("fcc", 4, 1)
+@pytest.mark.parametrize("name", ["741", "fcc256_0"])
+def test_default_cutoff_10A_every_atom(ctx, name, wg):
+    """compute_structure_betti_features at the reference's default r_cutoff = 10
+    (preprocess_betti.cpp:117; betti_features.cpp:103-119) for EVERY atom of 741.vasp (120 atoms,
+    ~300-point complexes) and of FCC-256 structure 0 (256 atoms, ~340 points), with the one-wave
+    (wg 0, the default) and the workgroup-per-complex (wg 1) wide kernels, against the
+    verbatim-Ripser fixtures: counts bit-exact, statistics within 1e-6."""
+    fx = np.load(os.path.join(GOLDEN, "rc10.npz"))
+    batch = _rc10_inputs(name)
+    if name == "fcc256_0":
+        assert np.array_equal(batch["positions"], fx["fcc256_0/positions"])  # generator bit-identity
     ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, wg)
     try:
         f, c = ctx.host_betti(batch, 10.0)
-        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 1 - wg)
-        f2, c2 = ctx.host_betti(batch, 10.0)
     finally:
         ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, WG_DEFAULT)
-    assert np.array_equal(c, c2)
-    np.testing.assert_allclose(f, f2, rtol=FEAT_RTOL, atol=FEAT_ATOL)
-    assert not np.isnan(f).any()
-    atoms = [0, 77, 200]
-    fo, co = O.ref_atom_betti(batch["lattice"][0], batch["positions"], batch["species"], 10.0, atoms)
-    assert np.array_equal(c[atoms], co), (c[atoms], co)
-    np.testing.assert_allclose(f[atoms], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
+    fo, co = fx[f"{name}/features"], fx[f"{name}/counts"]
+    assert f.shape == fo.shape and not np.isnan(f).any()
+    bad = np.nonzero((c != co).any(axis=1))[0]
+    assert bad.size == 0, (bad[:8], c[bad[:4]], co[bad[:4]])
+    np.testing.assert_allclose(f, fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
 
 
 def test_f32_instantiations_363_to_512_points(ctx):
@@ -116,9 +130,9 @@ def test_f32_fallback_matches_rank_codes(ctx):
 
 
 def test_workgroup_kernel_matches_wave_kernel(ctx):
-    """The workgroup-per-complex kernel (default for rank-coded 129..362-point complexes, distances
-    in LDS) and the one-wave-per-complex kernel (DGN_DEBUG_WIDE_WG = 0) give the same pairs and
-    counts; both against verbatim Ripser (ripser.cpp:514-1269)."""
+    """The workgroup-per-complex kernel (DGN_DEBUG_WIDE_WG = 1, off by default: rank-coded
+    129..362-point complexes, distances in LDS) and the default one-wave-per-complex kernel give
+    the same pairs and counts; both against verbatim Ripser (ripser.cpp:514-1269)."""
     rng = np.random.default_rng(47)
     sizes = [340, 200, 131, 90, 362]
     clouds = np.zeros((len(sizes), max(sizes), 3))

@@ -22,3 +22,17 @@ def test_generator_shapes_and_density():
     assert np.all(b["positions"][:256] > 0) and np.all(b["positions"][:256] < L)
     s = synth.make_batch("sc", 4, 1)
     assert abs(64 / s["lattice"][0, 0, 0] ** 3 - 0.0801) < 1e-3
+
+
+def test_rc10_fixture_inputs_match_generator():
+    """tests/golden/rc10.npz holds verbatim-Ripser outputs at 10 A for FCC-256 structure 0: its
+    stored positions are the generator's (so the GPU test feeds the same input), and its counts
+    are plausible (one essential dim-0 class per atom: every 10 A complex is connected)."""
+    import os
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "rc10.npz"))
+    b = synth.make_batch("fcc", 4, 1)
+    assert np.array_equal(fx["fcc256_0/positions"], b["positions"])
+    for name, n in (("fcc256_0", 256), ("741", 120)):
+        c = fx[f"{name}/counts"]
+        assert c.shape == (n, 4) and fx[f"{name}/features"].shape == (n, 35)
+        assert np.all(c[:, 1] == 1) and np.all(c[:, 2] > 0)
