@@ -129,16 +129,6 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
-// materialize a value in a VGPR here (stops the compiler from sinking select arms into
-// divergent branches; the arms below are cheap and computed unconditionally)
-__device__ __forceinline__ uint32_t pin(uint32_t x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ int pin(int x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
 // lanes [0, m) as a mask (m wave-uniform: scalar code). ballot(cmp) & lanes_below(m) keeps a
 // ballot to one v_cmp, where ballot(lane < m && cmp) materializes the combined bool first.
 __device__ __forceinline__ uint64_t lanes_below(int m) {
@@ -655,12 +645,17 @@ struct Complex {
                 colkey = uni64(sk[ci]);
                 tau = uni64(st[ci]);
             }
+            // the walk's state is wave-uniform; readfirstlane says so to the compiler, whose
+            // divergence analysis otherwise lets one vector-held value turn every branch of the
+            // walk into exec-masked code
+            colkey = uni64(colkey);
+            tau = uni64(tau);
             const uint32_t cp = key_packed(colkey);
             const float birth = key_diam(colkey);
             DGN_SUB(17);
-            int owner = find_pivot(npiv, tau);
+            int owner = (int)uni((uint32_t)find_pivot(npiv, tau));
             DGN_SUB(18);
-            uint32_t app = owner >= 0 ? kNone : (have_app ? app0 : apparent_owner_wave(dim, tau));
+            uint32_t app = uni(owner >= 0 ? kNone : (have_app ? app0 : apparent_owner_wave(dim, tau)));
             DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
 #ifdef DGN_PHASE_TIMING
@@ -708,12 +703,12 @@ struct Complex {
                         ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
                     }
 #endif
-                    tau = v > 0 ? pivot_of_V(dim, v, tau) : kInf;
+                    tau = uni64(v > 0 ? pivot_of_V(dim, v, tau) : kInf);
                     DGN_SUB(21);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
-                    owner = find_pivot(npiv, tau);
+                    owner = (int)uni((uint32_t)find_pivot(npiv, tau));
                     DGN_SUB(18);
-                    app = owner >= 0 ? kNone : apparent_owner_wave(dim, tau);
+                    app = uni(owner >= 0 ? kNone : apparent_owner_wave(dim, tau));
                     DGN_SUB(19);
                     if (owner < 0 && app == kNone) break;  // tau is this column's pivot
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
