@@ -946,7 +946,9 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                 const uint64_t low = lane < n ? (s.adj[lane] & ((lane == 0) ? 0ull : ((1ull << lane) - 1ull))) : 0ull;
                 const int c = __popcll(low);
                 const int inc = wave_inclusive_sum(c);
-                n_edges = __shfl(inc, kWave - 1, kWave);
+                // readlane, not a shuffle: the count must be a scalar (a shuffle result is a
+                // vector value to the compiler, and every loop over the edges would be exec-masked)
+                n_edges = (int)uni((uint32_t)__builtin_amdgcn_readlane(inc, kWave - 1));
                 int off = inc - c;
                 uint64_t mm = low;
                 while (mm) {
