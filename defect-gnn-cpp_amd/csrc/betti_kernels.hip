@@ -141,25 +141,6 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, kWave);
     return ((uint64_t)hi << 32) | lo;
 }
-// min over the wave of a 64-bit key in two 32-bit stages: the high words (DPP row rotations +
-// 4 readlanes), then the low words of the lanes holding that high word
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xf, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xf, 0xf, false));
-    // row minima -> lane 63 by row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3): one readlane
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x142, 0xa, 0xf, false));
-    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x143, 0xc, 0xf, false));
-    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-    const uint32_t hi = (uint32_t)(v >> 32);
-    const uint32_t mh = wave_min_u32(hi);
-    const uint32_t ml = wave_min_u32(hi == mh ? (uint32_t)v : 0xFFFFFFFFu);
-    return ((uint64_t)mh << 32) | ml;
-}
-
 // F-order key: ascending key == Ripser's filtration order (diameter ascending, then the
 // combinatorial index DESCENDING, greater_diameter_or_smaller_index at ripser.cpp:318-324).
 // Vertex tuples packed 8 bits per vertex in descending order preserve the colex (index) order.

@@ -208,10 +208,10 @@ struct WideCx {
                 }
                 if (out && v < lfree) lfree = v;
             }
-            const uint64_t m = wave_min(lmin);
+            const uint64_t m = wave_min_u64(lmin);
             int v;
             if (m == kInfW) {  // new component: lowest vertex outside the forest
-                v = wave_min(lfree);
+                v = (int)wave_min_u32((uint32_t)lfree);
                 ++n_inf0;
             } else {
                 const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
@@ -248,7 +248,7 @@ struct WideCx {
         int off = 0;
         for (int i = 1; i < n; ++i)
             for (int w = 0; 64 * w < i; ++w) {
-                uint64_t bits = aw(i, w);
+                uint64_t bits = uniw64(aw(i, w));  // one LDS word: uniform (scalar count below)
                 const int lim = i - 64 * w;
                 if (lim < 64) bits &= (1ull << lim) - 1ull;
                 if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = pack_edge(i, 64 * w + lane);
@@ -854,9 +854,9 @@ struct WideCx {
                 }
                 if (i < cnt) eval(rlw(vl, i), rlw(vd, i));
             }
-            const uint64_t m = wave_min(lmin);
+            const uint64_t m = wave_min_u64(lmin);
             if (m == kInfW) return kInfW;
-            const int cnt = wave_sum(lmin == m ? lcnt : 0);
+            const int cnt = (int)wave_sum_u32(lmin == m ? (uint32_t)lcnt : 0u);
             if (cnt & 1) {
                 const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
                 tv = rlw64(lp, l);

@@ -76,6 +76,37 @@ __device__ __forceinline__ T wave_inclusive_sum(T v) {
     return v;
 }
 
+// Wave reductions to a SCALAR: DPP row rotations (every lane of a 16-lane row gets the row's
+// result), row_bcast:15 / row_bcast:31 carry rows 0..2 into row 3, and one v_readlane of lane 63.
+// The result is uniform to the compiler; a __shfl-based reduction is a vector value to it, and a
+// branch on one turns every later branch on data derived from it into exec-masked code.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x128, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x142, 0xa, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// 64-bit minimum in two 32-bit stages: the high words, then the low words of the lanes holding
+// the minimal high word
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 32);
+    const uint32_t mh = wave_min_u32(hi);
+    const uint32_t ml = wave_min_u32(hi == mh ? (uint32_t)v : 0xFFFFFFFFu);
+    return ((uint64_t)mh << 32) | ml;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 __device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
 // One-wave LDS hand-off: a wave's LDS instructions execute in order, so lane-to-lane exchange
