@@ -1,9 +1,12 @@
 // preprocess_betti — batch driver equivalent to reference src/preprocess/preprocess_betti.cpp:30-143.
-//   preprocess_betti [raw_path processed_path [r_cutoff [n_pca_components [batch_structures]]]]
+//   preprocess_betti [--resume] [raw_path processed_path [r_cutoff [n_pca_components [batch_structures]]]]
 // Scans raw_path/*.vasp, orders ids "X_Y" by (X, Y) (:21-28,43-46), computes the N x 35 Betti
 // features of every structure, writes processed_path/betti/<id>.bin (save_betti_features format),
 // fits the PCA over all atoms and writes processed_path/pca_model.bin. Structures are sent to the
 // GPU in batches (one dgn_host_betti call per batch) instead of one OpenMP loop per structure.
+// --resume: a structure whose betti/<id>.bin already exists is loaded (load_betti_features) instead
+// of recomputed and its file is left untouched, as the Python upstream skips existing outputs
+// (.reference_code/Defect_GNN/Betti_number.py:208-209); the PCA is still fitted over every atom.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -29,11 +32,19 @@ static std::pair<int, int> parse_structure_id(const std::string& id) {
 
 static void log(const std::string& msg) { std::fprintf(stderr, "[preprocess_betti] %s\n", msg.c_str()); }
 
-int main(int argc, char** argv) {
+int main(int argc_in, char** argv_in) {
     std::string raw_path = "data/raw/defective_structures", processed_path = "data/processed";
     double r_cutoff = 10;
     int n_pca = 6;
     size_t batch = 1024;
+    bool resume = false;
+    std::vector<char*> args;
+    for (int i = 0; i < argc_in; ++i) {
+        if (i > 0 && std::string(argv_in[i]) == "--resume") resume = true;
+        else args.push_back(argv_in[i]);
+    }
+    const int argc = static_cast<int>(args.size());
+    char** argv = args.data();
     if (argc >= 3) {
         raw_path = argv[1];
         processed_path = argv[2];
@@ -56,21 +67,39 @@ int main(int argc, char** argv) {
         const auto t0 = std::chrono::steady_clock::now();
         std::vector<dgn::MatrixXd> all;
         size_t total_atoms = 0;
+        size_t skipped = 0;
         for (size_t lo = 0; lo < ids.size(); lo += batch) {
             const size_t hi = std::min(ids.size(), lo + batch);
             std::vector<crystal::Structure> st;
-            st.reserve(hi - lo);
-            for (size_t i = lo; i < hi; ++i) st.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
+            std::vector<size_t> todo;  // ids[i] to compute in this batch
+            std::vector<dgn::MatrixXd> feats(hi - lo);
+            for (size_t i = lo; i < hi; ++i) {
+                const std::string out = processed_path + "/betti/" + ids[i] + ".bin";
+                if (resume && fs::exists(out)) {
+                    feats[i - lo] = topology::load_betti_features(out);
+                    ++skipped;
+                } else {
+                    todo.push_back(i);
+                }
+            }
+            st.reserve(todo.size());
+            for (size_t i : todo) st.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
             std::vector<const crystal::Structure*> ptrs;
             for (const auto& s : st) ptrs.push_back(&s);
-            std::vector<dgn::MatrixXd> feats = topology::compute_batch_betti_features(ptrs, r_cutoff);
+            if (!ptrs.empty()) {
+                std::vector<dgn::MatrixXd> got = topology::compute_batch_betti_features(ptrs, r_cutoff);
+                for (size_t t = 0; t < todo.size(); ++t) {
+                    topology::save_betti_features(processed_path + "/betti/" + ids[todo[t]] + ".bin", got[t]);
+                    feats[todo[t] - lo] = std::move(got[t]);
+                }
+            }
             for (size_t i = lo; i < hi; ++i) {
-                topology::save_betti_features(processed_path + "/betti/" + ids[i] + ".bin", feats[i - lo]);
                 total_atoms += static_cast<size_t>(feats[i - lo].rows());
                 all.push_back(std::move(feats[i - lo]));
             }
             log("[" + std::to_string(hi) + "/" + std::to_string(ids.size()) + "] structures done");
         }
+        if (resume) log("resume: " + std::to_string(skipped) + " existing betti/<id>.bin loaded, not recomputed");
         const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         log("Betti features: " + std::to_string(ids.size()) + " structures, " + std::to_string(total_atoms) +
             " atoms in " + std::to_string(secs) + " s");

@@ -68,7 +68,6 @@ constexpr uint32_t kErrPiv = 1u << 3;
 constexpr uint32_t kErrPairs = 1u << 4;
 constexpr uint32_t kErrR = 1u << 5;
 [[maybe_unused]] constexpr uint32_t kErrOrder = 1u << 6;  // -DDGN_ORDER_CHECK builds
-[[maybe_unused]] constexpr uint32_t kErrExec = 1u << 8;   // -DDGN_EXEC_CHECK builds
 constexpr uint32_t kErrCapacity = kErrWorkCol | kErrNA | kErrPiv | kErrPairs | kErrR;
 
 // scratch layout per wave (bytes)
@@ -242,11 +241,11 @@ struct Complex {
     __device__ bool is_tree(int i, int j) const { return s.par[i] == j || s.par[j] == i; }
     // clearing marks live in the triangle min-cofacet table (scratch) until the dim-2 pass
     __device__ bool is_cleared(int a, int b, int c) const {
-        return sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] == kMcCleared;
+        return at(sp<uint8_t>(ScratchLayout::mincof), tri_dense(a, b, c)) == kMcCleared;
     }
-    __device__ void set_cleared(int a, int b, int c) { sp<uint8_t>(ScratchLayout::mincof)[tri_dense(a, b, c)] = kMcCleared; }
+    __device__ void set_cleared(int a, int b, int c) { at(sp<uint8_t>(ScratchLayout::mincof), tri_dense(a, b, c)) = kMcCleared; }
     __device__ void set_cleared_lane(int a, int b, int c) {
-        sp<uint8_t>(ScratchLayout::mincof)[tri_dense_lane(a, b, c)] = kMcCleared;
+        at(sp<uint8_t>(ScratchLayout::mincof), tri_dense_lane(a, b, c)) = kMcCleared;
     }
     __device__ uint8_t* mincof_of(int dim) const {
         return sp<uint8_t>(dim == 1 ? ScratchLayout::mincof_e : ScratchLayout::mincof);
@@ -261,7 +260,7 @@ struct Complex {
         int& np = dim == 1 ? n_p1 : n_p2;
         if (emit) {
             const int slot = np + mask_prefix(bal);
-            if (slot < kPairCap) pairs(dim)[slot] = make_float2(birth, death);
+            if (slot < kPairCap) at(pairs(dim), slot) = make_float2(birth, death);
         }
         np += __popcll(bal);
     }
@@ -353,7 +352,7 @@ struct Complex {
     // cleared triangles hold kNone), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
         const uint32_t f = uni(max_facet(dim, uni64(tau)));
-        const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
+        const uint32_t m = at(mincof_of(dim), col_dense(dim, f));
         return uni(m) == extra_vertex(key_packed(tau), f) ? f : kNone;
     }
 
@@ -377,7 +376,7 @@ struct Complex {
         const uint64_t* sp_piv = sp<uint64_t>(ScratchLayout::piv);
         for (int base = 2 * kWave; base < npiv; base += kWave) {
             const int i = base + lane;
-            bal = ballot(i < npiv && sp_piv[i] == tau);
+            bal = ballot(i < npiv && at(sp_piv, i) == tau);
             if (bal) return base + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
@@ -385,7 +384,7 @@ struct Complex {
     __device__ uint32_t piv_meta(int i) const {
         if (i < kWave) return rl(pm0, i);
         if (i < 2 * kWave) return rl(pm1, i - kWave);
-        return uni(sp<uint32_t>(ScratchLayout::vmeta)[i]);
+        return uni(at(sp<uint32_t>(ScratchLayout::vmeta), i));
     }
     __device__ void piv_push(int i, uint64_t tau, uint32_t meta) {
         const int lane = lane_id();
@@ -395,7 +394,7 @@ struct Complex {
             if (lane == i - kWave) { pk1 = tau; pm1 = meta; }
         } else if (lane == 0) {
             sp<uint64_t>(ScratchLayout::piv)[i] = tau;
-            sp<uint32_t>(ScratchLayout::vmeta)[i] = meta;
+            at(sp<uint32_t>(ScratchLayout::vmeta), i) = meta;
         }
     }
 
@@ -547,7 +546,7 @@ struct Complex {
     // F-minimal cofacet (recorded for every column by the lane-parallel pass)
     __device__ uint32_t apparent_owner_lane(int dim, uint64_t tau) const {
         const uint32_t f = max_facet(dim, tau);
-        const uint32_t m = mincof_of(dim)[col_dense(dim, f)];
+        const uint32_t m = at(mincof_of(dim), col_dense(dim, f));
         return m == extra_vertex(key_packed(tau), f) ? f : kNone;
     }
 
@@ -570,8 +569,8 @@ struct Complex {
         uint64_t* sk = sp<uint64_t>(ScratchLayout::sna_key);
         uint64_t* st = sp<uint64_t>(ScratchLayout::sna_tau);
         if (regs) {
-            if (lane < nna) { rk0 = gk[lane]; rt0 = gt[lane]; }
-            if (lane + kWave < nna) { rk1 = gk[lane + kWave]; rt1 = gt[lane + kWave]; }
+            if (lane < nna) { rk0 = at(gk, lane); rt0 = at(gt, lane); }
+            if (lane + kWave < nna) { rk1 = at(gk, lane + kWave); rt1 = at(gt, lane + kWave); }
             // rank by column key DESCENDING (Ripser processes columns in decreasing F-order)
             int r0 = 0, r1 = 0;
             const int n0 = nna < kWave ? nna : kWave;
@@ -668,7 +667,7 @@ struct Complex {
                             for (int t0 = 0; t0 < len && ok; t0 += kWave) {
                                 const int t = t0 + lane;
                                 uint32_t w = 0;
-                                if (t < len) w = gvstore[off + t];
+                                if (t < len) w = at(gvstore, off + t);
                                 const int cnt = len - t0 < kWave ? len - t0 : kWave;
                                 for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(dim, rl(w, u), v);
                             }
@@ -704,7 +703,7 @@ struct Complex {
             if (death > birth) {
                 if (lane == 0) {
                     const int slot = dim == 1 ? n_p1 : n_p2;
-                    if (slot < kPairCap) pairs(dim)[slot] = make_float2(birth, death);
+                    if (slot < kPairCap) at(pairs(dim), slot) = make_float2(birth, death);
                 }
                 if (dim == 1) ++n_p1;
                 else ++n_p2;
@@ -721,7 +720,7 @@ struct Complex {
                 if (vused + v > kVStoreCap || v > 511) { err |= kErrR; return; }
                 for (int t = lane; t < v; t += kWave) {
                     const uint32_t x = t < kWave ? vs0 : vs1;
-                    gvstore[vused + t] = x;
+                    at(gvstore, vused + t) = x;
                 }
                 meta = ((uint32_t)vused << 9) | (uint32_t)v;
                 vused = (int)uni((uint32_t)(vused + v));
@@ -757,11 +756,6 @@ struct Complex {
 template <int NP>
 __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
-#ifdef DGN_OCC_PAD
-    // A/B diagnostics only: extra LDS per wave to lower the occupancy (occupancy sensitivity)
-    __shared__ uint32_t occ_pad[DGN_OCC_PAD];
-    if (lane_id() == 0) occ_pad[blockIdx.x % DGN_OCC_PAD] = 0u;
-#endif
 #ifdef DGN_PHASE_TIMING
     // diagnostics counters in LDS (registers would change the kernel's occupancy)
     __shared__ uint64_t ph[32];
@@ -777,19 +771,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
     // complexes of this launch: all of them, or the overflow list written by the bucket pass
     const int64_t total = bl.work_list ? (int64_t)*bl.work_len : A;
     for (;;) {
-#ifdef DGN_EXEC_CHECK
-        // diagnostics: every lane must be live at the dequeue
-        {
-            const uint64_t ex = __builtin_amdgcn_read_exec();
-            if (ex != ~0ull) {
-                if (lane == __ffsll((unsigned long long)ex) - 1) {
-                    atomicOr(bl.error_flag, kErrExec);
-                    printf("DGN_EXEC_CHECK: exec %016lx at the dequeue (block %d)\n", (unsigned long)ex, (int)blockIdx.x);
-                }
-                return;
-            }
-        }
-#endif
         // Wave-uniform dequeue without a branch on the lane: every lane adds (lane == 0) to the
         // queue (one atomic after the compiler's wave combine) and lane 0's ticket is read back
         // with v_readlane into an SGPR, so the loop exit and everything keyed on the complex (gi,
@@ -816,7 +797,13 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             // 1/count(species) weight (betti_features.cpp:62-63, 77), from the distance pass
             const double weight = bl.weight ? bl.weight[gi] : 1.0;
 
-            Complex<NP> cx{s, n, bl.thr, scratch, 0u, 0, 0, 0, 0, 0, 0};
+            // the scratch base re-enters through an empty asm (scalar constraint: still uniform)
+            // per complex, so per-lane scratch addresses are formed at their uses as scalar base +
+            // vector offset instead of being hoisted out of the dequeue loop as 64-bit vector
+            // pointers, which the compiler then spills
+            uint8_t* cscr = scratch;
+            asm volatile("" : "+s"(cscr));
+            Complex<NP> cx{s, n, bl.thr, cscr, 0u, 0, 0, 0, 0, 0, 0};
 #ifdef DGN_PHASE_TIMING
             cx.ph = ph;
             cx.tprev = &t_prev;
@@ -835,7 +822,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int t = t0 + u * kWave + lane;
-                        v[u] = t < tot ? L[t] : 0.0f;
+                        v[u] = t < tot ? at(L, t) : 0.0f;
                     }
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
@@ -916,7 +903,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         if (k < best) { best = k; parent = v; }
                     }
                 }
-                if (lane < cx.n_d0) d0s[lane] = death;
+                if (lane < cx.n_d0) at(d0s, lane) = death;
                 if (lane < NP) s.par[lane] = (lane < n && !root) ? (uint8_t)parent : (uint8_t)0xFF;
             }
             lds_sync();
@@ -935,7 +922,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                 while (mm) {
                     const int j = __ffsll((unsigned long long)mm) - 1;
                     mm &= mm - 1;
-                    edges[off++] = (uint16_t)((lane << 8) | j);
+                    at(edges, off++) = (uint16_t)((lane << 8) | j);
                 }
             }
             __syncthreads();  // edge list (global scratch) visible to every lane
@@ -985,31 +972,31 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                                 mc = (uint32_t)bk;
                             }
                         }
-                        if (!dfr) mincof_e[edge_dense(i, j)] = (uint8_t)mc;
+                        if (!dfr) at(mincof_e, edge_dense(i, j)) = (uint8_t)mc;
                     }
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
                         if (slot < kNACap) {
-                            na_key[slot] = colkey;
-                            na_tau[slot] = best;
+                            at(na_key, slot) = colkey;
+                            at(na_tau, slot) = best;
                         }
                     }
                     nna += __popcll(bal);
                     const uint64_t bd = ballot(dfr);
-                    if (dfr) defer[ndef + mask_prefix(bd)] = ed;
+                    if (dfr) at(defer, ndef + mask_prefix(bd)) = ed;
                     ndef += __popcll(bd);
                 };
                 for (int base = 0; base < n_edges; base += kWave) {
                     const int e = base + lane;
-                    edge_col(e < n_edges, e < n_edges ? (uint32_t)edges[e] : 0u, kAppSteps);
+                    edge_col(e < n_edges, e < n_edges ? (uint32_t)at(edges, e) : 0u, kAppSteps);
                 }
                 if (ndef) {
                     __syncthreads();  // the deferred list (scratch) is read by other lanes
                     const int nd = ndef;
                     for (int base = 0; base < nd; base += kWave) {
                         const int e = base + lane;
-                        edge_col(e < nd, e < nd ? defer[e] : 0u, 1 << 20);
+                        edge_col(e < nd, e < nd ? at(defer, e) : 0u, 1 << 20);
                     }
                 }
                 __syncthreads();
@@ -1027,7 +1014,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             }
             if (!(dim_max >= 2 && cx.err == 0) && n >= 3) {
                 // no dim-2 pass to consume them: erase every triangle entry (clearing marks)
-                for (int t = lane; t < c3(n); t += kWave) mincof[t] = kMcNone;
+                for (int t = lane; t < c3(n); t += kWave) at(mincof, t) = kMcNone;
                 __syncthreads();
             }
             // ---- dim 2: one lane per column (uncleared triangle) ----
@@ -1046,8 +1033,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     // lane shuffle instead of a dependent scratch load (edges without a c < b in
                     // common refill again at once)
                     int wbase = 0;
-                    uint32_t win = lane < n_edges ? (uint32_t)edges[lane] : 0u;
-                    uint32_t win_next = kWave + lane < n_edges ? (uint32_t)edges[kWave + lane] : 0u;
+                    uint32_t win = lane < n_edges ? (uint32_t)at(edges, lane) : 0u;
+                    uint32_t win_next = kWave + lane < n_edges ? (uint32_t)at(edges, kWave + lane) : 0u;
                     while (true) {
                         while (true) {  // refill lanes with empty masks
                             const bool need = tmask == 0;
@@ -1068,7 +1055,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                                 wbase += kWave;
                                 win = win_next;
                                 const int t = wbase + kWave + lane;
-                                win_next = t < n_edges ? (uint32_t)edges[t] : 0u;
+                                win_next = t < n_edges ? (uint32_t)at(edges, t) : 0u;
                             }
                             if (ballot(tmask == 0) == 0) break;
                         }
@@ -1078,7 +1065,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         if (active) {
                             const int c = __ffsll((unsigned long long)tmask) - 1;
                             tmask &= tmask - 1;
-                            tl[ntri + mask_prefix(bal)] = pack3(ea, eb, c);
+                            at(tl, ntri + mask_prefix(bal)) = pack3(ea, eb, c);
                         }
                         ntri += __popcll(bal);
                     }
@@ -1118,7 +1105,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                                 mc = (uint32_t)bk;
                             }
                         }
-                        if (!dfr) mincof[tri_dense_lane(a, b, c)] = (uint8_t)mc;
+                        if (!dfr) at(mincof, tri_dense_lane(a, b, c)) = (uint8_t)mc;
                     }
 #ifdef DGN_PHASE_TIMING
                     // lane efficiency of the round-synchronous walk: steps summed over lanes [29],
@@ -1138,35 +1125,35 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
                         if (slot < kNACap) {
-                            na_key[slot] = colkey;
-                            na_tau[slot] = best;
+                            at(na_key, slot) = colkey;
+                            at(na_tau, slot) = best;
                         }
                     }
                     nna += __popcll(bal);
                     const uint64_t bd = ballot(dfr);
-                    if (dfr) defer[ndef + mask_prefix(bd)] = tp;
+                    if (dfr) at(defer, ndef + mask_prefix(bd)) = tp;
                     ndef += __popcll(bd);
                 };
-                uint32_t tp1 = lane < ntri ? tl[lane] : 0u;
-                uint32_t cl1 = lane < ntri ? (uint32_t)mincof[tri_dense_lane((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)] : 0u;
-                uint32_t tp2 = kWave + lane < ntri ? tl[kWave + lane] : 0u;
+                uint32_t tp1 = lane < ntri ? at(tl, lane) : 0u;
+                uint32_t cl1 = lane < ntri ? (uint32_t)at(mincof, tri_dense_lane((tp1 >> 16) & 255, (tp1 >> 8) & 255, tp1 & 255)) : 0u;
+                uint32_t tp2 = kWave + lane < ntri ? at(tl, kWave + lane) : 0u;
                 for (int base = 0; base < ntri; base += kWave) {
                     const uint32_t tp = tp1, clb = cl1;
                     const bool active = base + lane < ntri;
                     tp1 = tp2;
                     cl1 = base + kWave + lane < ntri
-                              ? (uint32_t)mincof[tri_dense_lane((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255)]
+                              ? (uint32_t)at(mincof, tri_dense_lane((tp2 >> 16) & 255, (tp2 >> 8) & 255, tp2 & 255))
                               : 0u;
-                    tp2 = base + 2 * kWave + lane < ntri ? tl[base + 2 * kWave + lane] : 0u;
+                    tp2 = base + 2 * kWave + lane < ntri ? at(tl, base + 2 * kWave + lane) : 0u;
                     tri_col(active, tp, clb, kAppSteps);
                 }
                 if (ndef) {
                     __syncthreads();  // the deferred list (scratch) is read by other lanes
                     const int nd = ndef;
-                    uint32_t tq = lane < nd ? defer[lane] : 0u;
+                    uint32_t tq = lane < nd ? at(defer, lane) : 0u;
                     for (int base = 0; base < nd; base += kWave) {
                         const uint32_t tp = tq;
-                        tq = base + kWave + lane < nd ? defer[base + kWave + lane] : 0u;
+                        tq = base + kWave + lane < nd ? at(defer, base + kWave + lane) : 0u;
                         // deferred columns are never cleared
                         tri_col(base + lane < nd, tp, 0u, 1 << 20);
                     }
@@ -1188,44 +1175,27 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
-#ifdef DGN_HANG_REPRO
-            // diagnostics only (tools/hang_repro.sh): the round-2 form that hung with the LDS-slot
-            // dequeue (the kernel-side forced retry and a `continue` right after the lane-0
-            // append); with the uniform dequeue it is an ordinary scalar branch
-            if (bl.force_retry) cx.err |= kErrNA;
-            const uint32_t err = uni(cx.err);
-            if (err && bl.retry_list && (err & kErrCapacity) == err) {
-                if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
-                continue;
-            }
-            if (err) {
-#else
             const uint32_t err = uni(cx.err);
             if (err && bl.retry_list && (err & kErrCapacity) == err) {
                 // workspace overflow: the capacity-retry launch (betti_wide_kernel, big layout)
                 // reduces this complex again and writes its outputs
                 if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
             } else if (err) {
-#endif
                 if (lane == 0) atomicOr(bl.error_flag, err);
-                if (feat && lane < 35) feat[lane] = __builtin_nan("");
-                if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
+                if (feat && lane < 35) at(feat, lane) = __builtin_nan("");
+                if (bl.counts && lane < 4) at(bl.counts + 4 * gi, lane) = -1;
             } else {
                 // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
                 const double myval = betti_stats35(d0s, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
-                if (feat && lane < 35) feat[lane] = myval;
+                if (feat && lane < 35) at(feat, lane) = myval;
                 if (bl.pairs_out) {
                     float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;
-                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) po[i] = make_float2(0.0f, d0s[i]);
-                    for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) po[bl.pair_cap + i] = cx.pairs(1)[i];
-                    for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) po[2 * bl.pair_cap + i] = cx.pairs(2)[i];
+                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) at(po, i) = make_float2(0.0f, at(d0s, i));
+                    for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) at(po, bl.pair_cap + i) = at(cx.pairs(1), i);
+                    for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) at(po, 2 * bl.pair_cap + i) = at(cx.pairs(2), i);
                 }
-                if (bl.counts && lane == 0) {
-                    bl.counts[4 * gi + 0] = cx.n_d0;
-                    bl.counts[4 * gi + 1] = cx.n_inf0;
-                    bl.counts[4 * gi + 2] = cx.n_p1;
-                    bl.counts[4 * gi + 3] = cx.n_p2;
-                }
+                if (bl.counts && lane < 4)  // #dim0 finite, #dim0 infinite, #dim1, #dim2
+                    at(bl.counts + 4 * gi, lane) = lane == 0 ? cx.n_d0 : (lane == 1 ? cx.n_inf0 : (lane == 2 ? cx.n_p1 : cx.n_p2));
             }
             lds_sync();
             DGN_PHASE(6);
@@ -1322,11 +1292,7 @@ __global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int n
     const bool tier48 = gi < bl.num_atoms && n > np_small && n <= np_mid;
     const bool mid = gi < bl.num_atoms && n > np_mid && n <= 64;
     // above kWideRegular points: straight to the retry list (rank-coded BIG launch)
-#ifdef DGN_HANG_REPRO
-    const bool huge = false;  // diagnostics: the regular wide launch meets them (its skip path)
-#else
     const bool huge = gi < bl.num_atoms && n > kWideRegular && bl.retry_list;
-#endif
     const bool wide = gi < bl.num_atoms && n > 64 && !huge;
     bucket_append(huge, bl.retry_list, bl.retry_len, gi);
     bucket_append(tier48, bl.mid_list, bl.mid_len, gi);

@@ -62,16 +62,10 @@ __device__ __forceinline__ uint64_t uniw64(uint64_t x) {
 }
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 // lane-to-lane hand-off through this wave's global scratch in the reduction's hot loop (V list,
-// pivot table, V store). The default is the workgroup barrier (its fence waits for every
-// outstanding global access of the wave, vmcnt(0)); -DDGN_WIDE_WAVE_FENCE uses a wavefront-scope
-// fence instead (A/B: a wave's own vector memory accesses are kept in order)
-__device__ __forceinline__ void wave_scratch_sync() {
-#ifdef DGN_WIDE_WAVE_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#else
-    __syncthreads();
-#endif
-}
+// pivot table, V store): the workgroup barrier, whose fence waits for every outstanding global
+// access of the wave (vmcnt(0)); a wavefront-scope fence instead measured 22.5 -> 21.9
+// structures/s at 10 A (round 3), so the barrier stays
+__device__ __forceinline__ void wave_scratch_sync() { __syncthreads(); }
 
 // combinatorial index of a packed simplex with nv vertices
 // insert vertex x (not in p) into a packed simplex of nv vertices
@@ -1000,7 +994,9 @@ struct WideCx {
     }
 
     // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) + outputs ----
-    __device__ void finish(int64_t gi, double weight) {
+    // true when the complex's outputs were written (false: listed for the retry launch, or an
+    // error with NaN outputs)
+    __device__ bool finish(int64_t gi, double weight) {
         const int lane = lane_id();
         double* feat = bl.features ? bl.features + 35 * gi : nullptr;
         if (n_p1 > ly.p_cap || n_p2 > ly.p_cap) err |= kEPairs;
@@ -1008,13 +1004,13 @@ struct WideCx {
             // workspace overflow: listed for the capacity-retry launch (betti_wide_layout big),
             // which writes this complex's outputs
             if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
-            return;
+            return false;
         }
         if (err) {
             if (lane == 0) atomicOr(bl.error_flag, err);
             if (feat && lane < 35) feat[lane] = __builtin_nan("");
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
-            return;
+            return false;
         }
         const float* d0s = sp<float>(ly.d0);
         const float2* P1 = sp<float2>(ly.p1);
@@ -1033,9 +1029,10 @@ struct WideCx {
             bl.counts[4 * gi + 2] = n_p1;
             bl.counts[4 * gi + 3] = n_p2;
         }
+        return true;
     }
 
-    __device__ void run(int64_t gi, int64_t slot, double weight) {
+    __device__ bool run(int64_t gi, int64_t slot, double weight) {
 #ifdef DGN_PHASE_TIMING
         // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
         uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -1079,10 +1076,11 @@ struct WideCx {
             for (int64_t t = lane_id(); t < nt; t += kWave) mc_t[t] = kMcNoneW;
         }
         __syncthreads();
-        finish(gi, weight);
+        const bool ok = finish(gi, weight);
         __syncthreads();
         WSTAMP(6);
 #undef WSTAMP
+        return ok;
     }
 };
 
@@ -1105,14 +1103,6 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
         if (wi >= total) break;
         const int64_t gi = (int64_t)(int32_t)uniw((uint32_t)bl.wide_list[wi]);
         const int n = (int)uniw((uint32_t)bl.npoints[gi]);
-#ifdef DGN_HANG_REPRO
-        // diagnostics only (tools/hang_repro.sh): the round-2 skip that hung with the LDS-slot
-        // dequeue; with the uniform dequeue above it is an ordinary scalar branch
-        if (n > ly.nmax && bl.retry_list) {
-            if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
-            continue;
-        }
-#endif
         // complexes above kWideRegular points never reach the regular launch (the bucket pass lists
         // them for the rank-coded retry launch); a larger one here is outside the layout
         if (n > ly.nmax) {
@@ -1122,8 +1112,9 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
         } else {
             WideCx<KW, MODE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
             if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
-            cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
-            if (bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
+            // dgn_debug_retry_count counts the complexes a retry launch reduced successfully
+            const bool ok = cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
+            if (ok && bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
         }
     }
 }

@@ -268,7 +268,6 @@ int take_betti_flag(dgn_ctx* c) {
         return fail(c, DGN_ERR_INTERNAL, "Betti neighbour search disagreed with the count pass (flags " + std::to_string(g) + ")");
     if (f & 1u) return fail(c, DGN_ERR_UNSUPPORTED, "local complex exceeds the kernel's point envelope");
     if (f & 64u) return fail(c, DGN_ERR_INTERNAL, "reduction order check failed");
-    if (f & 256u) return fail(c, DGN_ERR_INTERNAL, "partial EXEC mask at a Betti dequeue (DGN_EXEC_CHECK build)");
     return fail(c, DGN_ERR_CAPACITY, "per-complex workspace overflow, flags " + std::to_string(f));
 }
 

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dgn {
 
 constexpr int kWave = 64;  // CDNA wavefront; never 32
@@ -32,6 +34,20 @@ struct StructMeta {
 };
 
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+
+// element i of a per-wave scratch array as (scalar base) + (32-bit byte offset): the load/store
+// takes the base in SGPRs and one vector offset register (global_* vN, s[base]) instead of a
+// 64-bit vector address built per access (every scratch array here is far below 4 GB)
+template <class T>
+__device__ __forceinline__ T& at(T* base, uint32_t i) {
+    return *reinterpret_cast<T*>(reinterpret_cast<uint8_t*>(const_cast<std::remove_const_t<T>*>(base)) +
+                                 i * (uint32_t)sizeof(T));
+}
+template <class T>
+__device__ __forceinline__ const T& at(const T* base, uint32_t i) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const uint8_t*>(base) + i * (uint32_t)sizeof(T));
+}
+
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
@@ -251,8 +267,8 @@ __device__ __forceinline__ double betti_stats35(const float* d0, int n0, const f
         const float2* P = g <= 3 ? P1 : P2;
         const int which = g == 0 ? 1 : (g - 1) % 3;  // 0 persistence, 1 birth, 2 death (dims 1, 2)
         auto val = [&](int i) -> double {
-            if (g == 0) return (double)d0[i];
-            const float2 pr = P[i];
+            if (g == 0) return (double)at(d0, i);
+            const float2 pr = at(P, i);
             return which == 0 ? (double)pr.y - (double)pr.x : (which == 1 ? (double)pr.x : (double)pr.y);
         };
         double sm = 0.0, mx = -INFINITY, mn = INFINITY;

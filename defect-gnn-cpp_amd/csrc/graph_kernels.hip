@@ -867,19 +867,9 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     // stage view without positions (for_block_atoms<false> stores fx and the offset table only)
     const StageView st{nullptr, nullptr, nullptr, lds(fx_s), reinterpret_cast<DGN_LDS f64x4*>(lds(offt_s)), kStage};
     CountAcc acc;
-#if defined(DGN_COUNT1_PROBE) && DGN_COUNT1_PROBE == 2
-    // diagnostics builds only (tools/count_probe.py; wrong counts): no staging, no search
-    if (threadIdx.x < g.qa) cnt_s[threadIdx.x] = 0, nw_s[threadIdx.x] = 0;
-    __syncthreads();
-#else
     for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         const double* gp = P.gpos;
-#if defined(DGN_COUNT1_PROBE) && DGN_COUNT1_PROBE == 1
-        // diagnostics builds only: staging without the search
-        const int m = (int)st.fx[li].x & 1;
-        (void)gp;
-#else
         const int m = count_one_image(
             M, st.fx, st.offt,
             [&](int jj, double p[3]) __attribute__((always_inline)) {
@@ -888,14 +878,12 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
                 p[2] = gp[3 * jj + 2];
             },
             li, g.rc2, lds(mask_s[t]));
-#endif
         if (lane == 0) {
             cnt_s[t] = (int32_t)m;
             nw_s[t] = (M.natoms + 63) / 64;
         }
         acc.add(m, M.natoms, g.kmax);
     });
-#endif
     count_tile_store(g, tile, acc, out, counts, block_sums, block_aux, mask_out);
 }
 
@@ -1295,11 +1283,7 @@ __device__ __forceinline__ void rbf_stream_wave(T* __restrict__ out, int ne, con
             // bytes): plain stores, which the L2 merges into full lines -- measured on the fused
             // emit, config-4 shard: f64 4.01 -> 3.46 ms with plain stores, f32 2.23 -> 2.37 ms
             // (worse) with them (tools/r03_graph_exp.sh)
-#ifdef DGN_RBF_PLAIN_STORE
-            constexpr bool plain = true;
-#else
             constexpr bool plain = sizeof(T) == 8;
-#endif
             if constexpr (plain) *reinterpret_cast<vec_t*>(ob + V * v) = val;
             else __builtin_nontemporal_store(val, reinterpret_cast<vec_t*>(ob + V * v));
         }
@@ -1352,11 +1336,7 @@ __device__ __forceinline__ void rbf_direct(T* __restrict__ out, int total, const
             if constexpr (sizeof(T) == 4) t = k ? t + rs.dr : -de;
             else t = (double)k * rs.dr - de;
         }
-#ifdef DGN_RBF_PLAIN_STORE
-        *reinterpret_cast<vec_t*>(out + f) = o;
-#else
         __builtin_nontemporal_store(o, reinterpret_cast<vec_t*>(out + f));
-#endif
     }
     const int t0 = head + V * nvec;
     if (t0 + tix < total) out[t0 + tix] = one(t0 + tix);
@@ -1486,16 +1466,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             for (int i = threadIdx.x; i < ne; i += kGraphBlock) dl[i] = dist[e0 + i];
             __syncthreads();
         }
-#ifdef DGN_RBF_DIRECT
-        // A/B: every 16-byte unit computed straight into registers (no LDS staging): f32 with
-        // v_exp_f32 per value, f64 with the bounded Taylor exp per value
-        if (rs.dtype == 1)
-            rbf_direct(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne * rs.nbins, dl, rs);
-        else
-            rbf_direct(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne * rs.nbins, dl, rs);
-        EMIT_STAMP(4);
-        return;
-#endif
         if (rs.dtype == 1)
             rbf_stream_wave(reinterpret_cast<float*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
                             reinterpret_cast<DGN_LDS float*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
@@ -1566,12 +1536,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                     ok = inr && d2 < g.rc2;
                     kd[lane] = sqrt(d2);  // neighbor_list.cpp:53
                     kj[lane] = pack_jimg(j, n[0], n[1], n[2]);
-#ifdef DGN_EMIT_DEBUG
-                    if (!ok)
-                        printf("fast miss gi=%ld li=%d j=%d m=%d n=%d,%d,%d inr=%d d2=%.17g rc2=%.17g fq=%x,%x,%x,%x fj=%x,%x,%x,%x\n",
-                               (long)gi, li, j, m, n[0], n[1], n[2], (int)inr, d2, g.rc2, P.st.fx[li].x, P.st.fx[li].y,
-                               P.st.fx[li].z, P.st.fx[li].w, P.st.fx[j].x, P.st.fx[j].y, P.st.fx[j].z, P.st.fx[j].w);
-#endif
                 }
                 if (ballot(!ok)) {
                     if (lane == 0) atomicOr(error_flag, kGErrMissedHit);
@@ -1596,12 +1560,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         const int kept = (int)(row_start[t + 1] - rs0);
         if (m > CAP || kept != (m < K ? m : K)) {
             if (lane == 0) atomicOr(error_flag, m > CAP ? kGErrCap : kGErrMismatch);
-#ifdef DGN_EMIT_DEBUG
-            if (lane == 0)
-                printf("emit mismatch gi=%ld b=%ld t=%d m=%d kept=%d fast=%d natoms=%d staged=%d one=%d w0=%lx w1=%lx\n",
-                       (long)gi, (long)b, t, m, kept, (int)fast, M.natoms, (int)P.staged, M.one,
-                       (unsigned long)(mk ? mk[0] : 0), (unsigned long)(mk ? mk[1] : 0));
-#endif
             return;
         }
         wave_lds_sync();
@@ -1627,11 +1585,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         if (m <= kWave) {
             if (lane >= m && lane < ((m + 7) & ~7)) kd[lane] = __builtin_inf();  // rank_small reads groups of 8
             wave_lds_sync();
-#ifdef DGN_EMIT_NORANK
-            const int r = lane;  // A/B diagnostics only: rows in search order
-#else
             const int r = rank_small(kd, kj, m, lds(claim[w]));
-#endif
             if (lane < m) put(r, kd[lane], kj[lane]);
         } else {
             rank_large(kd, kj, m, put);
@@ -1900,58 +1854,14 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
                                (size_t)ly.total, s, g, stage, nwm, counts, block_offsets, row_ptr, col, dist, disp, rbf,
                                rs, error_flag, tl);
     };
-#ifdef DGN_EMIT_NORBF
-    go({0, nt, 0, 0, 0});  // A/B diagnostics only: rows without the RBF
-    return;
-#endif
     if (!STREAM || rs.dtype == 0 || !rbf) {
         go({0, nt, 0, 0, 0});
         return;
     }
-    // A/B diagnostics builds only (-DDGN_EMIT_PIPELINE / -DDGN_EMIT_SPLIT); never the environment
-#ifdef DGN_EMIT_PIPELINE
-    constexpr bool pipeline = true;
-#else
-    constexpr bool pipeline = false;
-#endif
-#ifdef DGN_EMIT_SPLIT
-    constexpr bool split = true;
-#else
-    constexpr bool split = false;
-#endif
-    if (split) {  // diagnostics: all rows, then all RBF (two launches)
-        go({0, nt, 0, 0, 0});
-        go({0, 0, 0, nt, 0});
-        return;
-    }
-    if (!pipeline) {
-        go({0, nt, 0, 0, 1});  // each block: rows, then its RBF
-        return;
-    }
-    // Pipeline (DGN_EMIT_PIPELINE=1, measured slower on MI355X: RBF blocks alone stream at ~4 TB/s
-    // and take slots from the row blocks): launch i writes the rows of chunk i and the RBF of
-    // chunk i - 1 (its rows complete at the launch boundary). Chunks: 1/16 at both ends (the
-    // unpaired head and tail), 2/16 in between.
-    constexpr int kParts = 16;
-    int64_t bnd[10];
-    int nb = 0;
-    bnd[nb++] = 0;
-    if (nt >= 4 * kParts) {
-        for (int p = 1; p < kParts; p += 2) bnd[nb++] = nt * p / kParts;
-    }
-    bnd[nb++] = nt;
-    for (int i = 0; i < nb; ++i) {
-        EmitTiles tl{0, 0, 0, 0, 0};
-        if (i + 1 < nb) {
-            tl.row0 = bnd[i];
-            tl.nrow = bnd[i + 1] - bnd[i];
-        }
-        if (i > 0) {
-            tl.rbf0 = bnd[i - 1];
-            tl.nrbf = bnd[i] - bnd[i - 1];
-        }
-        go(tl);
-    }
+    // one launch, each block writes its rows, then its tile's RBF (round 3 A/B: all rows then all
+    // RBF in two launches, and a chunk pipeline overlapping rows of chunk i with the RBF of chunk
+    // i - 1, were both slower: RBF-only blocks stream at ~4 TB/s and take slots from row blocks)
+    go({0, nt, 0, 0, 1});
 }
 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
@@ -1959,11 +1869,7 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
                              double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
     const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
-#ifdef DGN_EMIT_FLAT
-    const bool stream = false;  // A/B diagnostics: per-atom write_rbf_flat
-#else
     const bool stream = g.kmax <= (uint64_t)kStreamMaxK;
-#endif
 #define DGN_EMIT(C)                                                                                              \
     case C:                                                                                                      \
         if (stream) launch_emit_t<C, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, \

@@ -43,6 +43,12 @@ const char* dgn_status_string(int status);
 /* ---- context -------------------------------------------------------------------------- */
 typedef struct dgn_ctx dgn_ctx;
 
+/* A context owns its device workspaces, grown on demand and kept until dgn_ctx_destroy. The first
+ * Betti pass with complexes of at most kWideRegular (512) points also allocates the device-driven
+ * capacity-retry workspace once: up to 64 big-layout waves within a fixed 4 GB budget (about 4 GB at
+ * 64 points), whether or not any complex overflows, so that later passes never wait for the host;
+ * several contexts on one GPU each hold their own. Per-wave Betti scratch (narrow kernel ~1 MB per
+ * resident wave, wide kernel 15-60 MB per wave, at most half of the free HBM) is held the same way. */
 int dgn_ctx_create(int device, dgn_ctx** out);
 void dgn_ctx_destroy(dgn_ctx* ctx);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the context's own. */
@@ -56,8 +62,9 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  * DGN_DEBUG_WIDE_CAP     > 0: the wide launch's column / pivot / pair tables hold at most this many
  *                        entries (rounded up to a power of two), so ordinary complexes overflow in the
  *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps;
- * DGN_DEBUG_WIDE_WG      0 = one wave per rank-coded wide complex (betti_wide) instead of the default
- *                        workgroup per complex with its distances in LDS (129..362 points). */
+ * DGN_DEBUG_WIDE_WG      default 0: one wave per wide complex (betti_wide); 1 = the experimental
+ *                        workgroup-per-complex kernel with the u16 code triangle in LDS for rank-coded
+ *                        complexes of 129..362 points (betti_wg; measured slower, off by default). */
 enum {
     DGN_DEBUG_FORCE_RETRY = 1,
     DGN_DEBUG_WIDE_WAVES = 2,
@@ -171,9 +178,11 @@ int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* 
 int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
                    double* features, int32_t* counts);
 
-/* Fused step (device, asynchronous: no host synchronization for complexes of up to a few hundred
- * points -- larger ones size their capacity-retry workspace from one host read; errors are reported
- * by the next synchronizing call as for dgn_dev_betti): dgn_dev_graph_emit of a
+/* Fused step (device; no host synchronization while every local complex has at most 64 points, the
+ * 5 A path: the capacity-retry launch is device-driven. Complexes of 65..362 points (the wide tier,
+ * e.g. the reference's 10 A default) wait for the host twice: one read of the wide list's length for
+ * the rank-code slices and one of the retry list's length to size the retry workspace. Errors are
+ * reported by the next synchronizing call as for dgn_dev_betti): dgn_dev_graph_emit of a
  * preceding dgn_dev_graph_count, then dgn_dev_betti on the same batch. When the Betti cutoff equals
  * the graph cutoff (and epsilon is the default 1e-10) the Betti pass reuses the graph count's
  * per-atom neighbour counts and hit masks instead of searching a third time: CrystalGraph's

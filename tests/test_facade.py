@@ -180,19 +180,41 @@ def test_preprocess_driver(tmp_path, golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "libdgn_ref.so")),
-                    reason="verbatim Ripser (oracle/_ref) not built")
-def test_preprocess_driver_default_cutoff(tmp_path, golden):
+def test_preprocess_driver_default_cutoff(tmp_path):
     """preprocess_betti at the reference default r_cutoff = 10 (preprocess_betti.cpp:117):
-    ~300-point local complexes through the wide kernel; spot-check atoms of 741.vasp against
-    the verbatim Ripser (about 1 s per atom on one core)."""
-    import oracle_py as O
+    ~300-point local complexes through the wide kernel; every atom of 741.vasp against the
+    verbatim-Ripser fixture (tests/golden/rc10.npz, tests/golden/make_golden.py rc10)."""
     outdir = tmp_path / "processed10"
     rc, _, err = _run([os.path.join(BIN, "preprocess_betti"), POSCARS, str(outdir), "10", "6", "4"])
     assert rc == 0, err
     raw = open(outdir / "betti" / "741.bin", "rb").read()
     r, c = np.frombuffer(raw[:8], np.int32)
     feat = np.frombuffer(raw[8:], np.float64).reshape(r, c, order="F")
-    atoms = [0, 57]
-    fo, _ = O.ref_atom_betti(golden["741/lattice"], golden["741/positions"], golden["741/species"], 10.0, atoms)
-    np.testing.assert_allclose(feat[atoms], fo, rtol=1e-6, atol=1e-12)
+    fo = np.load(os.path.join(GOLDEN, "rc10.npz"))["741/features"]
+    assert feat.shape == fo.shape
+    np.testing.assert_allclose(feat, fo, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_preprocess_driver_resume(tmp_path, golden):
+    """--resume (the Python upstream's skip of existing outputs, Betti_number.py:208-209): a second
+    run leaves every existing betti/<id>.bin untouched, recomputes only a missing one (byte-identical
+    to the first run), and refits the same PCA from all atoms."""
+    outdir = tmp_path / "processed"
+    exe = os.path.join(BIN, "preprocess_betti")
+    rc, _, err = _run([exe, POSCARS, str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    bins = sorted(glob.glob(str(outdir / "betti" / "*.bin")))
+    first = {b: (open(b, "rb").read(), os.stat(b).st_mtime_ns) for b in bins}
+    pca1 = open(outdir / "pca_model.bin", "rb").read()
+    victim = str(outdir / "betti" / "741.bin")
+    os.remove(victim)
+    rc, _, err = _run([exe, "--resume", POSCARS, str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    assert "resume: 8 existing" in err
+    for b in bins:
+        data = open(b, "rb").read()
+        assert data == first[b][0], b
+        if b != victim:
+            assert os.stat(b).st_mtime_ns == first[b][1], b  # not rewritten
+    assert open(outdir / "pca_model.bin", "rb").read() == pca1

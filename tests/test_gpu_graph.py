@@ -184,8 +184,11 @@ def test_fcc256_cutoff_17A_above_1024_candidates(ctx):
     assert np.array_equal(g["dist"], dist)
     assert np.array_equal(g["disp"], disp)
     check_rbf(g["rbf"], dist, 17.0, 0.1)
-    with pytest.raises(Exception):
+    # without a neighbour cap the per-atom sorted-distance buffer holds at most 1,024 candidates:
+    # a loud DGN_ERR_UNSUPPORTED (status 5), not any other failure
+    with pytest.raises(dgn.DgnError) as e:
         ctx.host_graph(batch, abi.graph_params(r_cutoff=17.0, max_neighbors=None, rbf_cutoff=5.0, rbf_dr=0.1))
+    assert e.value.status == 5
 
 
 @pytest.mark.parametrize("k", [20, None])
