@@ -428,15 +428,28 @@ def cpu_baseline(args, sh, n_atoms, torch):
         col = sh.out["col"].cpu().numpy()
         dist = sh.out["dist"].cpu().numpy()
         g_ok = True
+        rbf_rel = 0.0
+        rbf_gpu = sh.out["rbf"]
         for s in (0, S - 1):
-            nl = O.neighbor_list(host["lattice"][s], host["positions"][s * n_atoms:(s + 1) * n_atoms], args.rc, args.k)
+            lat_s, pos_s = host["lattice"][s], host["positions"][s * n_atoms:(s + 1) * n_atoms]
+            nl = O.neighbor_list(lat_s, pos_s, args.rc, args.k)
             a, b = rp[s * n_atoms], rp[(s + 1) * n_atoms]
             g_ok = g_ok and np.array_equal(rp[s * n_atoms:(s + 1) * n_atoms + 1] - a, nl["row_ptr"]) and \
                 np.array_equal(col[a:b], nl["col"]) and np.array_equal(dist[a:b], nl["dist"])
+            # the timed shard's RBF rows of the same structures vs the oracle (gaussian_rbf,
+            # edge_features.cpp:7-24, one row per edge in CSR order)
+            ref = O.structure_graph(lat_s, pos_s, args.rc, args.k, args.rbf_rc, args.dr, want_rbf=True)
+            got = rbf_gpu[a:b].double().cpu().numpy()
+            if got.shape != ref.shape:
+                rbf_rel = float("inf")
+            else:
+                rbf_rel = max(rbf_rel, float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-300))))
         parity = {"betti_atoms_checked": int(S * n_atoms), "betti_counts_exact": bool(np.array_equal(cnt, ref_c)),
                   "betti_feat_max_rel": float(np.max(np.where(np.abs(ref_f) > 1e-12, rel, 0.0))),
                   "betti_feat_within_1e-6": bool(np.all((rel <= 1e-6) | (np.abs(feat - ref_f) <= 1e-12))),
                   "graph_structures_checked": 2, "graph_csr_bit_exact": bool(g_ok),
+                  "rbf_structures_checked": 2, "rbf_max_rel": rbf_rel,
+                  "rbf_within_tol": bool(rbf_rel <= (1e-12 if args.rbf_dtype == "f64" else 1e-6)),
                   "reference": "verbatim vendored Ripser (oracle/_ref) + restated neighbour list"}
     return base, parity
 
