@@ -8,7 +8,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
             -mllvm -amdgpu-atomic-optimizer-strategy=DPP
 LIB      := $(PKG)/lib/libdgn.so
 
-KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/betti_wg.o $(BUILD)/betti_rank.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o
+KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/betti_rank.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o
 
 all: $(LIB) facade oracle
 
@@ -61,7 +61,7 @@ $(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
 $(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp $(CSRC)/dgn_device.hpp
 	@mkdir -p $(DBUILD)
 	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -x hip -c $< -o $@
-$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/betti_wg.o $(DBUILD)/betti_rank.o $(DBUILD)/node_kernels.o $(DBUILD)/dgn_api.o
+$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/betti_rank.o $(DBUILD)/node_kernels.o $(DBUILD)/dgn_api.o
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 

@@ -38,7 +38,6 @@ namespace dgn {
 namespace {
 
 constexpr uint64_t kInfW = ~0ull;
-constexpr uint32_t kNoneW = 0xFFFFFFFFu;
 constexpr uint16_t kMcNoneW = 0xFFFF;     // not a column, or no cofacet
 constexpr uint16_t kMcClearedW = 0xFFFE;  // triangle is the pivot of a dim-1 column (clearing)
 constexpr uint64_t kLazyW = 1ull << 63;    // pivot meta: V = {column simplex} (packed, low bits)
@@ -75,18 +74,33 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 // BIG (complexes of 513..1024 points): vertices packed in 10 bits, distances replaced by their
 // rank codes in the complex (order- and equality-preserving, < 2^20; betti_rank_codes) so a
 // simplex key (code << 36) | ~index fits 64 bits (C(1024, 4) < 2^36); code -> f32 via the
-// complex's sorted distances. Otherwise 9-bit vertices and (f32 bits << 32) | ~index keys.
+// complex's sorted distances. HUGE (1025..2048 points): 11-bit vertices, codes < 2^22 and keys
+// (code << 40) | ~index (C(2048, 4) < 2^40); a packed triangle (33 bits) travels as a u64 and the
+// adjacency bitsets (n x 32 words) move from LDS to the wave's scratch. Otherwise 9-bit vertices
+// and (f32 bits << 32) | ~index keys.
 // MODE: kF32 (distances as f32 bits), kC16 (u16 rank codes: 4-byte -> 2-byte matrix for
-// complexes of <= 362 points, C(362, 2) < 2^16), kBig (above).
-constexpr int kF32 = 0, kC16 = 1, kBig = 2;
+// complexes of <= 362 points, C(362, 2) < 2^16), kBig, kHuge (above).
+constexpr int kF32 = 0, kC16 = 1, kBig = 2, kHuge = 3;
 template <int KW, int MODE>
 struct WideCx {
     static constexpr bool BIG = MODE == kBig;
+    static constexpr bool HUGE = MODE == kHuge;
     static constexpr bool CODED = MODE != kF32;
     static constexpr int kWW = KW;
-    static constexpr int VB = BIG ? 10 : 9;            // bits per packed vertex
+    static constexpr int VB = HUGE ? 11 : (BIG ? 10 : 9);  // bits per packed vertex
     static constexpr uint64_t VM = (1ull << VB) - 1;
-    static constexpr int KS = BIG ? 36 : 32;           // key: (distance code << KS) | ~index
+    static constexpr int KS = HUGE ? 40 : (BIG ? 36 : 32);  // key: (distance code << KS) | ~index
+    // a packed column simplex / V entry (edge or triangle, 3 VB bits)
+    using PT = std::conditional_t<HUGE, uint64_t, uint32_t>;
+    static constexpr PT kNoneP = ~PT(0);
+    __device__ static PT rlp(PT x, int l) {
+        if constexpr (HUGE) return rlw64(x, l);
+        else return rlw(x, l);
+    }
+    __device__ static PT unip(PT x) {
+        if constexpr (HUGE) return uniw64(x);
+        else return uniw(x);
+    }
     __device__ static int pv(uint64_t p, int field) { return (int)((p >> (VB * field)) & VM); }
     __device__ static uint64_t pidx(int nv, uint64_t p) {
         if (nv == 2) return bin2(pv(p, 1)) + pv(p, 0);
@@ -145,7 +159,8 @@ struct WideCx {
             if (MODE == kC16) D16[(int64_t)i * n + i] = 0;
             else D[(int64_t)i * n + i] = 0u;
         }
-        wave_lds_order();
+        if constexpr (HUGE) wave_scratch_sync();  // the zeroed bitsets (scratch) before the atomics
+        else wave_lds_order();
         for (int i = 1; i < n; ++i) {
             for (int j0 = 0; j0 < i; j0 += kWave) {
                 const int j = j0 + lane;
@@ -163,10 +178,15 @@ struct WideCx {
                     e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
                 }
                 const uint64_t b = ballot(e);
-                if (lane == 0) adj[i * W + (j0 >> 6)] = b;  // row i, columns j < i
+                if (lane == 0) {  // row i, columns j < i
+                    if constexpr (HUGE) atomicOr((unsigned long long*)&adj[i * W + (j0 >> 6)], b);
+                    else adj[i * W + (j0 >> 6)] = b;
+                }
                 if (e) atomicOr((unsigned long long*)&adj[j * W + (i >> 6)], 1ull << (i & 63));
             }
         }
+        // HUGE: the bitsets were built by L2 atomics; the agent-scope fence drops the CU's L1 copies
+        if constexpr (HUGE) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
         __syncthreads();
     }
 
@@ -324,7 +344,7 @@ struct WideCx {
     }
 
     // append a non-apparent column (lanes with `na`) to the scratch list
-    __device__ void na_append(bool na, int& nna, uint64_t colkey, uint64_t tau, uint64_t tv, uint32_t colp) {
+    __device__ void na_append(bool na, int& nna, uint64_t colkey, uint64_t tau, uint64_t tv, PT colp) {
         const uint64_t bal = ballot(na);
         if (na) {
             const int slot = nna + mask_prefix(bal);
@@ -332,7 +352,7 @@ struct WideCx {
                 sp<uint64_t>(ly.na_key)[slot] = colkey;
                 sp<uint64_t>(ly.na_tau)[slot] = tau;
                 sp<uint64_t>(ly.na_tv)[slot] = tv;
-                sp<uint32_t>(ly.na_col)[slot] = colp;
+                sp<PT>(ly.na_col)[slot] = colp;
             }
         }
         nna += __popcll(bal);
@@ -349,7 +369,7 @@ struct WideCx {
             const int e = base + lane;
             bool na = false;
             uint64_t colkey = 0, best = kInfW, bestp = 0;
-            uint32_t colp = 0;
+            PT colp = 0;
             if (e < n_edges) {
                 const uint32_t ed = edges[e];
                 const int i = (int)(ed >> VB), j = (int)(ed & VM);
@@ -402,7 +422,8 @@ struct WideCx {
         int c = 0, w = 0, bk = 0;
         uint64_t m = 0, tidx = 0;
         uint32_t bd = 0xFFFFFFFFu;  // diameter of the best cofacet of the lane's triangle so far
-        uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, colp = 0, hda = 0, hdb = 0, hdc = 0;
+        uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, hda = 0, hdb = 0, hdc = 0;
+        PT colp = 0;
         bool found = false;
 #ifdef DGN_PHASE_TIMING
         uint64_t nsteps = 0, niter = 0, ncols = 0;
@@ -439,7 +460,7 @@ struct WideCx {
                 tm &= tm - 1ull;
                 act = fresh = true;
                 tidx = bin3(ea) + bin2(eb) + c;
-                colp = ((uint32_t)ea << (2 * VB)) | ((uint32_t)eb << VB) | (uint32_t)c;
+                colp = ((PT)ea << (2 * VB)) | ((PT)eb << VB) | (PT)c;
                 w = W - 1;
                 m = aw(ea, w) & aw(eb, w) & aw(c, w);
                 bd = 0xFFFFFFFFu;
@@ -449,7 +470,7 @@ struct WideCx {
             if (!ballot(act)) break;
             bool na = false;
             uint64_t colkey = 0, ntau = kInfW, ntv = 0;
-            uint32_t ncolp = 0;
+            PT ncolp = 0;
             if (act) {
                 const int a = ea, b = eb;
                 // (2) one step: up to kStep candidates, highest first
@@ -564,7 +585,7 @@ struct WideCx {
         uint64_t* K = sp<uint64_t>(ly.na_key);
         uint64_t* T = sp<uint64_t>(ly.na_tau);
         uint64_t* V = sp<uint64_t>(ly.na_tv);
-        uint32_t* Cc = sp<uint32_t>(ly.na_col);
+        PT* Cc = sp<PT>(ly.na_col);
         for (int i = cnt + lane; i < N; i += kWave) K[i] = 0ull;  // padding sorts last
         __syncthreads();
         for (int k = 2; k <= N; k <<= 1)
@@ -577,7 +598,7 @@ struct WideCx {
                             K[i] = y;
                             K[l] = x;
                             const uint64_t t0 = T[i], v0 = V[i];
-                            const uint32_t c0 = Cc[i];
+                            const PT c0 = Cc[i];
                             T[i] = T[l];
                             V[i] = V[l];
                             Cc[i] = Cc[l];
@@ -638,44 +659,13 @@ struct WideCx {
         return false;
     }
 
-    // Apparent owner of the pivot tau (packed, dim + 2 vertices; whole wave, uniform): its F-max
-    // facet f if tau is f's F-minimal cofacet (recorded by the lane-parallel pass; tree edges and
-    // cleared triangles hold kMcNone), else kNone.
-    __device__ uint32_t apparent_owner(int dim, uint64_t tv) const {
-        const int nv = dim + 2;
-        int v[4];
-        for (int t = 0; t < nv; ++t) v[t] = pv(tv, nv - 1 - t);  // v[0] largest
-        uint32_t dd[4][4];
-        for (int s = 0; s < nv; ++s)
-            for (int t = s + 1; t < nv; ++t) dd[s][t] = uniw(d(v[s], v[t]));
-        uint64_t bestk = 0, bestf = 0;
-        int drop = 0;
-        for (int t = 0; t < nv; ++t) {  // facet without v[t]
-            uint32_t diam = 0;
-            uint64_t f = 0;
-            for (int s = 0; s < nv; ++s) {
-                if (s == t) continue;
-                f = (f << VB) | (uint64_t)v[s];
-                for (int u = s + 1; u < nv; ++u)
-                    if (u != t) diam = max(diam, dd[s][u]);
-            }
-            const uint64_t kk = wkey(diam, pidx(nv - 1, f));
-            if (kk > bestk) {
-                bestk = kk;
-                bestf = f;
-                drop = t;
-            }
-        }
-        const uint16_t m = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
-        return uniw(m) == (uint32_t)v[drop] ? (uint32_t)bestf : kNoneW;
-    }
-
     // Owner of the pivot tau in one round trip where possible: the first 64-slot window of the
     // pivot table (keys and metadata) and tau's edge lengths (lane p loads edge p) are loaded
-    // together; a table hit returns its metadata (app = kNone), otherwise the apparent owner is
-    // decided from the edge lengths already in registers and one min-cofacet table read
-    // (apparent_owner's logic). Returns kNoMetaW when tau is not in the table.
-    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, uint32_t& app) const {
+    // together; a table hit returns its metadata (app = kNone). Otherwise the apparent owner: tau's
+    // F-max facet f if tau is f's F-minimal cofacet (recorded by the lane-parallel pass; tree edges
+    // and cleared triangles hold kMcNone), decided from the edge lengths already in registers and
+    // one min-cofacet table read. Returns kNoMetaW when tau is not in the table.
+    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, PT& app) const {
         const int lane = lane_id();
         const uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint64_t* HM = sp<uint64_t>(ly.h_meta);
@@ -696,7 +686,7 @@ struct WideCx {
         const uint64_t hit = ballot(hk == tau), emp = ballot(hk == 0ull);
         const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
         const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
-        app = kNoneW;
+        app = kNoneP;
         if (fh < fe) return rlw64(hm, fh);
         if (fe == kWave) {  // the window was full: probe on (rare at load factor <= 1/2)
             const uint64_t m = hfind(tau);
@@ -740,27 +730,27 @@ struct WideCx {
         }
         const uint16_t m = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
         const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
-        if (uniw(m) == (uint32_t)vd) app = (uint32_t)bestf;
+        if (uniw(m) == (uint32_t)vd) app = (PT)bestf;
         return kNoMetaW;
     }
 
     // ---- the working column's V list (scratch: vlist[0..v), packed simplices, no small cap) ----
-    __device__ int v_find(uint32_t x, int v) const {
+    __device__ int v_find(PT x, int v) const {
         const int lane = lane_id();
-        const uint32_t* VL = sp<uint32_t>(ly.vlist);
+        const PT* VL = sp<PT>(ly.vlist);
         for (int base = 0; base < v; base += kWave) {
-            const uint32_t y = base + lane < v ? VL[base + lane] : kNoneW;
+            const PT y = base + lane < v ? VL[base + lane] : kNoneP;
             const uint64_t bal = ballot(y == x);
             if (bal) return base + __ffsll((unsigned long long)bal) - 1;
         }
         return -1;
     }
-    __device__ bool v_toggle(uint32_t x, int& v) {  // V ^= {x}; false on overflow
-        uint32_t* VL = sp<uint32_t>(ly.vlist);
+    __device__ bool v_toggle(PT x, int& v) {  // V ^= {x}; false on overflow
+        PT* VL = sp<PT>(ly.vlist);
         const int pos = v_find(x, v);
         if (pos >= 0) {
             if (pos != v - 1) {
-                const uint32_t last = uniw(VL[v - 1]);
+                const PT last = unip(VL[v - 1]);
                 if (lane_id() == 0) VL[pos] = last;
             }
             v = v - 1;
@@ -779,10 +769,10 @@ struct WideCx {
     // floor and repeat. Returns kInf for the zero column; tv = packed pivot.
     __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
         const int k = lane_id();
-        const uint32_t* VL = sp<uint32_t>(ly.vlist);
+        const PT* VL = sp<PT>(ly.vlist);
         // V entries and their diameters live in registers (lane i: entry base + i), read back with
         // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
-        const uint32_t vl0 = k < v ? VL[k] : 0u;
+        const PT vl0 = k < v ? VL[k] : PT(0);
         const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
 #ifdef DGN_PHASE_TIMING
         ++dg_searches;
@@ -793,7 +783,7 @@ struct WideCx {
 #endif
             uint64_t lmin = kInfW, lp = 0;
             int lcnt = 0;
-            auto eval = [&](uint32_t s, uint32_t ds) {
+            auto eval = [&](PT s, uint32_t ds) {
                 const int a = dim == 1 ? pv(s, 1) : pv(s, 2);
                 const int b = dim == 1 ? pv(s, 0) : pv(s, 1);
                 const int c = pv(s, 0);
@@ -827,26 +817,27 @@ struct WideCx {
                 }
             };
             for (int base = 0; base < v; base += kWave) {
-                uint32_t vl = vl0, vd = vd0;
+                PT vl = vl0;
+                uint32_t vd = vd0;
                 if (base > 0) {
-                    vl = base + k < v ? VL[base + k] : 0u;
+                    vl = base + k < v ? VL[base + k] : PT(0);
                     vd = base + k < v ? sdiam(dim, vl) : 0u;
                 }
                 const int cnt = v - base < kWave ? v - base : kWave;
                 int i = 0;
 #if DGN_PV_UNROLL >= 4
                 for (; i + 3 < cnt; i += 4) {  // four entries' distance reads in flight together
-                    eval(rlw(vl, i), rlw(vd, i));
-                    eval(rlw(vl, i + 1), rlw(vd, i + 1));
-                    eval(rlw(vl, i + 2), rlw(vd, i + 2));
-                    eval(rlw(vl, i + 3), rlw(vd, i + 3));
+                    eval(rlp(vl, i), rlw(vd, i));
+                    eval(rlp(vl, i + 1), rlw(vd, i + 1));
+                    eval(rlp(vl, i + 2), rlw(vd, i + 2));
+                    eval(rlp(vl, i + 3), rlw(vd, i + 3));
                 }
 #endif
                 for (; i + 1 < cnt; i += 2) {  // two entries' distance reads in flight together
-                    eval(rlw(vl, i), rlw(vd, i));
-                    eval(rlw(vl, i + 1), rlw(vd, i + 1));
+                    eval(rlp(vl, i), rlw(vd, i));
+                    eval(rlp(vl, i + 1), rlw(vd, i + 1));
                 }
-                if (i < cnt) eval(rlw(vl, i), rlw(vd, i));
+                if (i < cnt) eval(rlp(vl, i), rlw(vd, i));
             }
             const uint64_t m = wave_min_u64(lmin);
             if (m == kInfW) return kInfW;
@@ -892,8 +883,8 @@ struct WideCx {
         const uint64_t* K = sp<uint64_t>(ly.na_key);
         const uint64_t* T = sp<uint64_t>(ly.na_tau);
         const uint64_t* V = sp<uint64_t>(ly.na_tv);
-        const uint32_t* Cc = sp<uint32_t>(ly.na_col);
-        uint32_t* vstore = sp<uint32_t>(ly.vstore);
+        const PT* Cc = sp<PT>(ly.na_col);
+        PT* vstore = sp<PT>(ly.vstore);
         float2* pairs = sp<float2>(dim == 1 ? ly.p1 : ly.p2);
         int& np = dim == 1 ? n_p1 : n_p2;
         int npiv = 0;
@@ -902,28 +893,28 @@ struct WideCx {
             const uint64_t colkey = uniw64(K[ci]);
             uint64_t tau = uniw64(T[ci]);
             uint64_t tv = uniw64(V[ci]);
-            const uint32_t cp = uniw(Cc[ci]);
+            const PT cp = unip(Cc[ci]);
             const uint32_t birth = kdiam(colkey);
-            uint32_t app;
+            PT app;
             uint64_t meta = lookup(dim, tau, tv, app);
             WSUB(1);
             int v = 0;  // 0 = lazy: V == {this column}
-            if (meta != kNoMetaW || app != kNoneW) {
+            if (meta != kNoMetaW || app != kNoneP) {
                 v_toggle(cp, v);
                 int64_t guard = 0;
                 for (;;) {
                     bool ok = true;
-                    if (app != kNoneW) {
+                    if (app != kNoneP) {
                         ok = v_toggle(app, v);
                     } else if (meta & kLazyW) {
-                        ok = v_toggle((uint32_t)(meta & ~kLazyW), v);
+                        ok = v_toggle((PT)(meta & ~kLazyW), v);
                     } else {
                         const int64_t off = (int64_t)(meta >> kMetaLenBits);
                         const int len = (int)(meta & ((1ull << kMetaLenBits) - 1));
                         for (int t0 = 0; t0 < len && ok; t0 += kWave) {
-                            const uint32_t w = t0 + lane < len ? vstore[off + t0 + lane] : 0u;
+                            const PT w = t0 + lane < len ? vstore[off + t0 + lane] : PT(0);
                             const int cnt = len - t0 < kWave ? len - t0 : kWave;
-                            for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(rlw(w, u), v);
+                            for (int u = 0; u < cnt && ok; ++u) ok = v_toggle(rlp(w, u), v);
                         }
                     }
                     if (!ok) {
@@ -938,7 +929,7 @@ struct WideCx {
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
                     meta = lookup(dim, tau, tv, app);
                     WSUB(1);
-                    if (meta == kNoMetaW && app == kNoneW) break;  // tau is this column's pivot
+                    if (meta == kNoMetaW && app == kNoneP) break;  // tau is this column's pivot
                     if (++guard > ly.guard) {
                         err |= kEGuard;
                         break;
@@ -960,7 +951,7 @@ struct WideCx {
                     err |= kER;
                     break;
                 }
-                const uint32_t* VL = sp<uint32_t>(ly.vlist);
+                const PT* VL = sp<PT>(ly.vlist);
                 for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
                 wave_scratch_sync();
                 m = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
@@ -1088,12 +1079,14 @@ template <int KW, int MODE>
 __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const WideLayout& ly) {
     // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
     // [nmax] u16
+    // [nmax] u16 (HUGE: the parents only, the adjacency lives in the wave's scratch at ly.adj)
     extern __shared__ uint64_t wide_lds[];
+    constexpr bool kHugeMode = MODE == kHuge;
     const int64_t ww = (ly.nmax + 63) / 64;
-    uint64_t* adj = wide_lds;
-    uint16_t* par = reinterpret_cast<uint16_t*>(wide_lds + ly.nmax * ww);
     const int lane = lane_id();
     uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
+    uint64_t* adj = kHugeMode ? reinterpret_cast<uint64_t*>(scr + ly.adj) : wide_lds;
+    uint16_t* par = reinterpret_cast<uint16_t*>(kHugeMode ? wide_lds : wide_lds + ly.nmax * ww);
     const int64_t total = (int64_t)*bl.wide_len;
     for (;;) {
         // wave-uniform dequeue without a branch on the lane (see betti_kernels.hip): every lane adds
@@ -1149,11 +1142,13 @@ WideKernel wide_kernel_for(int nmax, bool c16) {
     if (w <= 4) return betti_wide_kernel<4, kF32>;
     if (w <= 6) return betti_wide_kernel<6, kF32>;
     if (w <= 8) return betti_wide_kernel<8, kF32>;
-    return betti_wide_kernel<16, kBig>;  // 513..1024 points: rank-coded distances (BIG)
+    if (w <= 16) return betti_wide_kernel<16, kBig>;  // 513..1024 points: rank-coded distances (BIG)
+    return betti_wide_kernel<32, kHuge>;              // 1025..2048 points: HUGE
 }
 
 size_t wide_lds_bytes(int nmax) {
     const int64_t ww = (nmax + 63) / 64;
+    if (nmax > kWideBigPoints) return (size_t)(8 * ((nmax + 3) / 4));  // parents only
     return (size_t)(8 * (nmax * ww + (nmax + 3) / 4));
 }
 
@@ -1161,27 +1156,28 @@ size_t wide_lds_bytes(int nmax) {
 
 // Scratch layout of one wave for complexes of up to nmax points (all offsets 256-B aligned).
 // big = the capacity-retry layout (complexes whose reduction outgrew the regular caps): column,
-// pivot and pair tables sized for every simplex of the complex, a 16M-entry V store.
-WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix) {
+// pivot and pair tables of 2^(base_log2 + 2 grow) entries (base_log2 = 24 but for tests), never
+// more than every simplex of the complex needs (C(nmax, 3) columns), and a V store of as many
+// entries. The host raises `grow` while complexes still overflow (kWideMaxGrow levels): a complex
+// outgrows the last level only when its tables exceed 2^(base_log2 + 6) entries.
+WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, int base_log2) {
     WideLayout l{};
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
-    int64_t cap = 1024;
-    // the big (capacity-retry) layout caps its column / pivot / pair tables at 2^24 entries and its
-    // V store at 2^24 words: a complex that outgrows even these (e.g. a dense clique of several
-    // hundred points, C(n, 3) > 2^24 above ~465 points) fails with DGN_ERR_CAPACITY
-    int64_t cap_max = big ? (int64_t(1) << 24) : (int64_t(1) << 17);
+    const bool huge = nmax > kWideBigPoints;
+    const int64_t pt = huge ? 8 : 4;  // bytes of a packed column simplex (HUGE: 33-bit triangles)
+    int64_t cap_max = big ? (int64_t(1) << (base_log2 + 2 * grow)) : (int64_t(1) << 17);
     if (!big && cap_limit > 0) {
         cap_max = 64;
         while (cap_max < cap_limit) cap_max <<= 1;
-        cap = cap_max < cap ? cap_max : cap;
     }
+    int64_t cap = std::min<int64_t>(1024, cap_max);
     while ((cap < t || cap < e) && cap < cap_max) cap <<= 1;
     l.nmax = nmax;
     l.na_cap = (int32_t)cap;
     l.p_cap = (int32_t)cap;
     l.h_cap = (int32_t)(2 * cap);
-    l.vs_cap = big ? (1 << 24) : (1 << 20);
+    l.vs_cap = big ? (int32_t)(int64_t(1) << (base_log2 + 2 * grow)) : (1 << 20);
     l.vl_cap = big ? (int32_t)std::min<int64_t>(cap, 1 << 22) : (1 << 16);
     l.guard = big ? (int64_t(1) << 32) : (int64_t(1) << 20);
     int64_t o = 0;
@@ -1190,18 +1186,18 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix)
         o = align256(o + bytes);
         return at;
     };
-    l.D = take(matrix ? 4 * n * n : 0);
-    l.wg = matrix ? 0 : 1;
-    l.mc_e = take(matrix ? 2 * e : 4 * e);
-    l.mc_t = take(matrix ? 2 * t : (t + 31) / 32 * 4);
+    l.D = take(4 * n * n);
+    l.mc_e = take(2 * e);
+    l.mc_t = take(2 * t);
     l.edges = take(4 * e);
+    l.adj = take(huge ? 8 * n * ((n + 63) / 64) : 0);
     l.na_key = take(8 * cap);
     l.na_tau = take(8 * cap);
     l.na_tv = take(8 * cap);
-    l.na_col = take(4 * cap);
+    l.na_col = take(pt * cap);
     l.na_perm = take(4 * cap);
-    l.vstore = take(4 * (int64_t)l.vs_cap);
-    l.vlist = take(4 * (int64_t)l.vl_cap);
+    l.vstore = take(pt * (int64_t)l.vs_cap);
+    l.vlist = take(pt * (int64_t)l.vl_cap);
     l.vdiam = take(4 * (int64_t)l.vl_cap);
     l.h_key = take(8 * 2 * cap);
     l.h_meta = take(8 * 2 * cap);
@@ -1216,9 +1212,7 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, bool matrix)
 hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves) {
     hipError_t e = hipMemset2DAsync(l.base + l.h_key, (size_t)l.total, 0, 8 * (size_t)l.h_cap, (size_t)waves, s);
     if (e != hipSuccess) return e;
-    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges; the workgroup
-    // layout's clearing bitset (mc_t .. edges) starts all zero
-    if (l.wg) return hipMemset2DAsync(l.base + l.mc_t, (size_t)l.total, 0, (size_t)(l.edges - l.mc_t), (size_t)waves, s);
+    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges
     return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
 }
 

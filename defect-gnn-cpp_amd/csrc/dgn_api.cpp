@@ -129,7 +129,8 @@ struct dgn_ctx {
     DevBuf bflags;                // [kBFWords] sticky Betti words (above)
     int big_nmax = 0, big_waves = 0;  // capacity-retry workspace (b_big) the tables were initialised for
     // betti workspace
-    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_big, b_rank, b_rscal, b_rank16, b_rscal16;
+    DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_rlist2, b_big, b_rank, b_rscal, b_rank16,
+        b_rscal16;
     int betti_slots = 0;
     bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
@@ -137,16 +138,16 @@ struct dgn_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int cus = 0;  // compute units of the device (device_cus)
     int wide_nmax = 0, wide_waves = 0, wide_cap = 0;  // layout the wide scratch's tables were initialised for
-    bool wide_wg = false;                             // ... and whether it is the workgroup kernel's
     // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
     bool dbg_force_retry = false;  // every complex of a Betti pass through the capacity-retry launch
     int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
     int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
-    bool dbg_wide_wg = false;      // workgroup-per-complex kernel for rank-coded 129..362-point complexes (unverified: off)
+    int dbg_big_log2 = 0;          // capacity-retry layout's first-level table size log2 (0 = natural 24)
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
     DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
+    DevBuf emit_keys;     // the large-row emit's per-wave key rows (graph_emit_cap == kEmitGlobalKeys)
 #ifdef DGN_PHASE_TIMING
     DevBuf phase;
     unsigned long long phase_host[32] = {0};
@@ -379,11 +380,15 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     if (!W.have || W.pos != b->positions || W.atoms != b->num_atoms)
         return fail(c, DGN_ERR_ARG, "dgn_dev_graph_emit: no matching dgn_dev_graph_count on this context");
     const int cap = graph_emit_cap(W.max_candidates, W.k);
-    if (cap == 0)
-        return fail(c, DGN_ERR_UNSUPPORTED,
-                    W.max_candidates > 2048 ? "more than 2048 neighbour candidates for one atom (cutoff too large)"
-                                            : "more than 1024 neighbour candidates for one atom needs max_neighbors <= 64");
     if (b->num_atoms == 0) return DGN_OK;
+    double* key_rows = nullptr;
+    if (cap == kEmitGlobalKeys) {
+        // rows of more candidates than the LDS holds (neighbor_list.cpp:27-66 has no cap): per-wave
+        // key rows in HBM for one chunk of tiles (~0.4 GB at 2,700 candidates), kept for reuse
+        HIP_TRY(c, c->emit_keys.ensure((size_t)emit_key_rows_per_chunk() * (size_t)emit_key_row_doubles(W.max_candidates) *
+                                       sizeof(double)));
+        key_rows = c->emit_keys.as<double>();
+    }
     Scalars* sc = c->scalars.as<Scalars>();
     HIP_TRY(c, hipMemsetAsync(&sc->graph_flag, 0, sizeof(uint32_t), c->stream));
     const GraphLaunch g = graph_launch(W, b, W.rc, W.eps, W.k, true);
@@ -402,7 +407,8 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     {
         TimedLaunch t(c, "graph_emit", bytes, 0);
         HIP_TRY(c, launch_graph_emit(c->stream, g, cap, stage, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
-                                     const_cast<int64_t*>(row_ptr), col, dist_rows, disp, rbf, rs, &sc->graph_flag));
+                                     const_cast<int64_t*>(row_ptr), col, dist_rows, disp, rbf, rs, &sc->graph_flag,
+                                     key_rows, W.max_candidates));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->emit_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     c->emit_pending = true;
@@ -473,14 +479,10 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
     WideLayout wl{};
     int wide_waves = 0;
-    // rank-coded wide complexes of 129..362 points (the 10 A path): one workgroup per complex with
-    // the code triangle in LDS (betti_wg.hip); wide_waves then counts workgroups
-    const bool use_wg = c->dbg_wide_wg && c->dbg_wide_c16 && max_points > 64 && max_points <= kC16MaxPoints &&
-                        betti_wg_supported(max_points);
     if (max_points > 64) {
         const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
-        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap, !use_wg);
-        // as many waves (workgroups) as the device keeps resident (dynamic LDS sized by
+        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap);
+        // as many waves as the device keeps resident (dynamic LDS sized by
         // max_points), each with its own scratch, within half of the free HBM (288 GB per MI355X;
         // at least 8 GB)
         size_t free_b = 0, total_b = 0;
@@ -488,16 +490,14 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
         const int64_t resident =
-            use_wg ? betti_wg_resident_blocks(c->device, wide_nmax)
-                   : betti_wide_resident_waves(c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
+            betti_wide_resident_waves(c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         if (c->dbg_wide_waves > 0 && c->dbg_wide_waves < wide_waves) wide_waves = c->dbg_wide_waves;  // A/B only
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
-        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap ||
-            c->wide_wg != use_wg) {
+        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap) {
             // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
             // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
             // restores both for the entries it used
@@ -505,7 +505,6 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             c->wide_nmax = wide_nmax;
             c->wide_waves = wide_waves;
             c->wide_cap = wl.na_cap;
-            c->wide_wg = use_wg;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
@@ -595,10 +594,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                     wb.rank_codes = codes;
                     wb.rank_sorted = sorted;
                     wb.rank_stride = rstride;
-                    if (use_wg)
-                        HIP_TRY(c, launch_betti_wg(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
-                    else
-                        HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
+                    HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
                 }
                 HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope
             }
@@ -627,7 +623,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             WideLayout big = betti_wide_layout(nmax, true);
             const int64_t fit = (int64_t(4) << 30) / big.total;
             const int64_t waves = std::min<int64_t>({fit, betti_wide_resident_waves(c->device, nmax), 64});
-            if (!coded && waves >= 8) {
+            if (!coded && waves >= 8 && c->dbg_big_log2 == 0) {
                 if (c->big_nmax != nmax || c->big_waves < waves) {
                     HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
                     big.base = c->b_big.as<uint8_t>();
@@ -659,63 +655,76 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        const int64_t nretry = c->host->s.retry_len;
+        int64_t nretry = c->host->s.retry_len;
         if (nretry == 0) return DGN_OK;
         // complexes above kWideRegular points (listed by the bucket pass) run on rank codes
-        // (betti_rank_codes, the BIG instantiation), in slices of at most 512 complexes
-        WideLayout big = betti_wide_layout(nmax, true);
+        // (betti_rank_codes, the BIG / HUGE instantiations), in slices of at most 512 complexes.
+        // The tables grow with the complexes (the reference's Ripser has no caps): a complex that
+        // outgrows level `grow` is listed again and reduced at the next level, 4x the tables
         c->big_nmax = 0;  // the workspace below is laid out per call
-        size_t free_b = 0, total_b = 0;
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+        HIP_TRY(c, c->b_rlist2.ensure(sizeof(int32_t) * (size_t)A));
+        int32_t* cur = c->b_rlist.as<int32_t>();
+        int32_t* nxt = c->b_rlist2.as<int32_t>();
         const int64_t rstride = ((int64_t)nmax * (nmax - 1) / 2 + 63) / 64 * 64;
-        const int64_t slice = coded ? std::min<int64_t>(nretry, 512) : nretry;
-        const size_t rank_bytes = coded ? betti_rank_temp_bytes(slice, rstride) + 8 * (size_t)slice * rstride : 0;
-        const int64_t budget = (int64_t)(free_b / 2) + (int64_t)c->b_big.bytes - (int64_t)rank_bytes;
-        const int64_t waves =
-            std::min<int64_t>({slice, budget / big.total, betti_wide_resident_waves(c->device, nmax)});
-        if (waves < 1)
-            return fail(c, DGN_ERR_CAPACITY, "capacity retry: no device memory for a " + std::to_string(big.total) +
-                                                 "-byte workspace");
-        HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
-        big.base = c->b_big.as<uint8_t>();
-        HIP_TRY(c, betti_wide_init_scratch(c->stream, big, (int)waves));
-        if (coded) {
-            HIP_TRY(c, c->b_rank.ensure(rank_bytes));
-            HIP_TRY(c, c->b_rscal.ensure(sizeof(uint32_t) * 2 * (size_t)((nretry + slice - 1) / slice)));
-        }
-        BettiLaunch rb = pb;
-        rb.rank_codes = nullptr;  // set per slice below when coded
-        rb.rank_sorted = nullptr;
-        rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
-        rb.retry_len = nullptr;
-        rb.force_retry = 0;
-        rb.retried = bflags + kBFRetried;
-        std::vector<uint32_t> lens;
-        for (int64_t r0 = 0; r0 < nretry; r0 += slice) {
-            const int64_t cnt = std::min<int64_t>(slice, nretry - r0);
-            rb.wide_list = c->b_rlist.as<int32_t>() + r0;
-            if (coded) {
-                uint32_t* codes = c->b_rank.as<uint32_t>();
-                uint32_t* sorted = codes + slice * rstride;
-                void* tmp = sorted + slice * rstride;
-                HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, rb.wide_list, cnt, rstride,
-                                            codes, sorted, tmp, rank_bytes - 8 * (size_t)slice * rstride));
-                rb.rank_codes = codes;
-                rb.rank_sorted = sorted;
-                rb.rank_stride = rstride;
-                uint32_t* sl = c->b_rscal.as<uint32_t>() + 2 * (r0 / slice);
-                lens.push_back((uint32_t)cnt);
-                HIP_TRY(c, hipMemsetAsync(sl, 0, 2 * sizeof(uint32_t), c->stream));
-                HIP_TRY(c, hipMemcpyAsync(sl, &lens.back(), sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` may reallocate
-                rb.wide_len = sl;
-                rb.wide_queue = sl + 1;
-            } else {
-                rb.wide_len = &sc->retry_len;
-                rb.wide_queue = &sc->retry_queue;
+        for (int grow = 0;; ++grow) {
+            const bool last = grow == kWideMaxGrow;
+            WideLayout big = betti_wide_layout(nmax, true, 0, grow, c->dbg_big_log2 ? c->dbg_big_log2 : 24);
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+            const int64_t slice = coded ? std::min<int64_t>(nretry, 512) : nretry;
+            const int64_t nsl = (nretry + slice - 1) / slice;
+            const size_t rank_bytes = coded ? betti_rank_temp_bytes(slice, rstride) + 8 * (size_t)slice * rstride : 0;
+            const int64_t budget =
+                (int64_t)(free_b / 2) + (int64_t)c->b_big.bytes + (int64_t)c->b_rank.bytes - (int64_t)rank_bytes;
+            const int64_t waves =
+                std::min<int64_t>({slice, budget / big.total, betti_wide_resident_waves(c->device, nmax)});
+            if (waves < 1)
+                return fail(c, DGN_ERR_CAPACITY, "capacity retry: no device memory for a " +
+                                                     std::to_string(big.total) + "-byte workspace");
+            HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
+            big.base = c->b_big.as<uint8_t>();
+            HIP_TRY(c, betti_wide_init_scratch(c->stream, big, (int)waves));
+            if (coded) HIP_TRY(c, c->b_rank.ensure(rank_bytes));
+            // per slice (length, queue), then the next level's list length
+            HIP_TRY(c, c->b_rscal.ensure(sizeof(uint32_t) * (2 * (size_t)nsl + 2)));
+            uint32_t* sl0 = c->b_rscal.as<uint32_t>();
+            uint32_t* next_len = sl0 + 2 * nsl;
+            std::vector<uint32_t> lens((size_t)nsl);
+            for (int64_t q = 0; q < nsl; ++q) lens[q] = (uint32_t)std::min<int64_t>(slice, nretry - q * slice);
+            HIP_TRY(c, hipMemsetAsync(sl0, 0, sizeof(uint32_t) * (2 * (size_t)nsl + 2), c->stream));
+            for (int64_t q = 0; q < nsl; ++q)
+                HIP_TRY(c, hipMemcpyAsync(sl0 + 2 * q, &lens[q], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+            BettiLaunch rb = pb;
+            rb.rank_codes = nullptr;  // set per slice below when coded
+            rb.rank_sorted = nullptr;
+            rb.retry_list = last ? nullptr : nxt;  // last level: a further overflow is DGN_ERR_CAPACITY
+            rb.retry_len = last ? nullptr : next_len;
+            rb.force_retry = 0;
+            rb.retried = bflags + kBFRetried;
+            for (int64_t q = 0; q < nsl; ++q) {
+                rb.wide_list = cur + q * slice;
+                if (coded) {
+                    uint32_t* codes = c->b_rank.as<uint32_t>();
+                    uint32_t* sorted = codes + slice * rstride;
+                    void* tmp = sorted + slice * rstride;
+                    HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, rb.wide_list,
+                                                (int64_t)lens[q], rstride, codes, sorted, tmp,
+                                                rank_bytes - 8 * (size_t)slice * rstride));
+                    rb.rank_codes = codes;
+                    rb.rank_sorted = sorted;
+                    rb.rank_stride = rstride;
+                }
+                rb.wide_len = sl0 + 2 * q;
+                rb.wide_queue = sl0 + 2 * q + 1;
+                TimedLaunch t(c, "betti_retry", 0.0, 0.0);
+                HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)std::min<int64_t>(waves, lens[q])));
             }
-            TimedLaunch t(c, "betti_retry", 0.0, 0.0);
-            HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)std::min<int64_t>(waves, cnt)));
+            HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, next_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope; the next level's count
+            nretry = last ? 0 : c->host->s.retry_len;
+            if (nretry == 0) break;
+            std::swap(cur, nxt);
         }
         // the regular wide layout's tables are not touched; the big buffer is kept for reuse
         HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
@@ -886,7 +895,7 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
         case DGN_DEBUG_WIDE_WAVES: c->dbg_wide_waves = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
         case DGN_DEBUG_WIDE_CAP: c->dbg_wide_cap = value > 0 ? value : 0; return DGN_OK;
-        case DGN_DEBUG_WIDE_WG: c->dbg_wide_wg = value != 0; return DGN_OK;
+        case DGN_DEBUG_BIG_LOG2: c->dbg_big_log2 = value > 0 && value < 24 ? value : 0; return DGN_OK;
         default: return fail(c, DGN_ERR_ARG, "dgn_ctx_set_debug: unknown knob " + std::to_string(knob));
     }
 }

@@ -65,11 +65,18 @@ hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t*
                              int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq,
                              uint32_t* max_natoms, unsigned long long* sum_m);
 // Fused emit: each block re-runs the search for its atoms, ranks, writes row_ptr / col / dist /
-// disp and the RBF. cap >= max candidates of the count pass (64..512); stage = atoms staged in LDS
-// (max structure size if <= kStage, else 0).
+// disp and the RBF. cap = graph_emit_cap(max candidates of the count pass, kmax): 64..2048 (the
+// per-wave hit lists in LDS) or kEmitGlobalKeys (rows of more candidates: key_rows, caller-owned,
+// emit_key_rows_per_chunk() rows of emit_key_row_doubles(max_candidates) doubles); stage = atoms
+// staged in LDS (max structure size if <= kStage, else 0).
+constexpr int kEmitGlobalKeys = -1;
+constexpr int64_t kEmitGkChunkBlocks = 2048;  // tiles per launch of the global-key emit
+int64_t emit_key_row_doubles(uint32_t max_candidates);
+int64_t emit_key_rows_per_chunk();
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
-                             double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag);
+                             double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag,
+                             double* key_rows = nullptr, uint32_t max_candidates = 0);
 
 hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out);
 
@@ -82,7 +89,7 @@ inline int graph_tile_atoms(int64_t num_atoms, int cus) {
     while (qa > 4 && graph_blocks(num_atoms, qa) < 8 * (int64_t)cus) qa >>= 1;
     return qa;
 }
-int graph_emit_cap(uint32_t max_candidates, uint64_t kmax);  // 0 if unsupported
+int graph_emit_cap(uint32_t max_candidates, uint64_t kmax);  // LDS cap, or kEmitGlobalKeys
 
 // ---- Betti ----
 struct BettiLaunch {
@@ -139,35 +146,29 @@ struct BettiLaunch {
     int64_t rank_stride;
 };
 // wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout. Up to
-// kWideRegular points in the regular launch; above it (rank-coded, 10-bit vertices) in the retry
-// launch after betti_rank_codes
-constexpr int kWideMaxPoints = 1024;
+// kWideRegular points in the regular launch; above it (rank-coded: 10-bit vertices up to
+// kWideBigPoints, 11-bit vertices and the adjacency in scratch above) in the retry launch after
+// betti_rank_codes
+constexpr int kWideMaxPoints = 2048;
+constexpr int kWideBigPoints = 1024;
 constexpr int kWideRegular = 512;
 constexpr int kC16MaxPoints = 362;  // C(362, 2) < 2^16: u16 rank codes (wide launch)
+constexpr int kWideMaxGrow = 3;     // capacity-retry layout levels: tables of 2^24 .. 2^30 entries
 struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
     int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
-    int32_t wg;     // workgroup-kernel layout (matrix = false): mc_e = cleared-triangle list (u32 per
-                    // edge), mc_t = clearing bitset (a bit per triangle, starts and ends all zero)
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
-    int64_t D, mc_e, mc_t, edges, na_key, na_tau, na_tv, na_col, na_perm, vstore, vlist, vdiam, h_key, h_meta, h_used, p1, p2,
-        d0;
+    int64_t D, mc_e, mc_t, edges, adj, na_key, na_tau, na_tv, na_col, na_perm, vstore, vlist, vdiam, h_key, h_meta,
+        h_used, p1, p2, d0;
 };
 // cap_limit > 0 (tests, DGN_DEBUG_WIDE_CAP): the regular layout's column / pivot / pair tables
 // hold at most cap_limit entries, so ordinary complexes overflow in the kernel and take the
 // capacity-retry path
-// matrix = false: no per-wave distance matrix (the workgroup kernel keeps it in LDS)
-WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0, bool matrix = true);
+// grow (big only, 0..kWideMaxGrow): the capacity-retry level, tables of 2^(base_log2 + 2 grow) entries
+WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0, int grow = 0, int base_log2 = 24);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
 int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // device-wide resident waves (occupancy API)
-// workgroup-per-complex kernel (betti_wg.hip) for rank-coded complexes of 129..kC16MaxPoints points:
-// the u16 code triangle and the adjacency in LDS, scratch per workgroup (betti_wide_layout with
-// matrix = false); b.rank_codes / b.rank_sorted required
-bool betti_wg_supported(int nmax);
-size_t betti_wg_lds_bytes(int nmax);
-int betti_wg_resident_blocks(int device, int nmax);
-hipError_t launch_betti_wg(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int blocks);
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
 // occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
 // equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,

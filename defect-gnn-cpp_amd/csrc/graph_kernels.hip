@@ -1065,9 +1065,10 @@ __device__ __forceinline__ int rank_small(const DGN_LDS double* kd, const DGN_LD
     }
     return r;
 }
-// m > 64: lane s ranks entries s, s + 64, ... with the full key (broadcast LDS reads)
-template <class Visit>
-__device__ __forceinline__ void rank_large(const DGN_LDS double* kd, const DGN_LDS uint64_t* kj, int m, Visit&& visit) {
+// m > 64: lane s ranks entries s, s + 64, ... with the full key (broadcast reads; LDS, or the
+// global key rows of the large-row emit)
+template <class PD, class PJ, class Visit>
+__device__ __forceinline__ void rank_large(PD kd, PJ kj, int m, Visit&& visit) {
     for (int s = lane_id(); s < m; s += kWave) {
         const double d = kd[s];
         const uint64_t j = kj[s];
@@ -1108,9 +1109,9 @@ __device__ __forceinline__ void rbf_split(int f, const RbfSpec& r, int& e, int& 
 // Write the RBF of `total` = edges x nbins flat values starting at `out` from the edge distances
 // sd[] with `threads` cooperating threads (thread index tix): scalar head to a 16-byte boundary,
 // non-temporal 16-byte body (written once, never re-read here), scalar tail.
-template <typename T>
-__device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, const DGN_LDS double* sd, const RbfSpec& rs,
-                                               int tix, int threads) {
+template <typename T, class PS>
+__device__ __forceinline__ void write_rbf_flat(T* __restrict__ out, int total, PS sd, const RbfSpec& rs, int tix,
+                                               int threads) {
     constexpr int V = 16 / sizeof(T);
     const int nb = rs.nbins;
     const int mis = (int)(((uintptr_t)out / sizeof(T)) & (V - 1));
@@ -1371,7 +1372,7 @@ __host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool s
     l.keyd = take(kW * cap * 8);
     l.keyj = take(kW * cap * 8);
     l.mask = take(kQA * nwm * 8);
-    l.sorted = take(stream ? 0 : kW * (cap + 1) * 8);
+    l.sorted = take(stream || cap == 0 ? 0 : kW * (cap + 1) * 8);
     const int a_end = o;
     l.gm = rbf_stream_geom(nb > 0 ? nb : 1, elem > 0 ? elem : 4);
     l.wbytes = (stream && nb > 0) ? rbf_stream_buf_bytes(l.gm, nb, elem > 0 ? elem : 4) : 0;
@@ -1411,6 +1412,15 @@ struct EmitTiles {
     int fused;
 };
 
+// CAP = 0 (kEmitGlobalKeys, rows of more candidates than the LDS instantiations hold): each wave's
+// hit list, keys and sorted distances live in its own global row, [3 cap + 1] doubles at
+// base + (block of the launch * kW + wave) * (3 cap + 1); the host launches the tiles in chunks so
+// the rows stay bounded
+struct EmitKeys {
+    double* base;
+    int32_t cap;
+};
+
 template <int CAP, bool STREAM>
 __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, int stage_cap, int nwm,
                                                                   const int32_t* __restrict__ counts,
@@ -1419,7 +1429,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                                                                   int32_t* __restrict__ col, double* __restrict__ dist,
                                                                   double* __restrict__ disp, void* __restrict__ rbf,
                                                                   RbfSpec rs, uint32_t* __restrict__ error_flag,
-                                                                  EmitTiles tl) {
+                                                                  EmitTiles tl, EmitKeys gk) {
+    constexpr bool GK = CAP == 0;
     extern __shared__ double dyn[];
     __shared__ uint32_t ring[kW][kRing];
     __shared__ uint8_t claim[kW][kWave];
@@ -1430,13 +1441,31 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     DGN_LDS uint8_t* base = reinterpret_cast<DGN_LDS uint8_t*>(lds(dyn));
     const StageView st = make_stage(reinterpret_cast<double*>(dyn) + ly.stage / 8, stage_cap, nullptr);
     DGN_LDS double* dl = reinterpret_cast<DGN_LDS double*>(base + ly.dl);
-    DGN_LDS double* key_d = reinterpret_cast<DGN_LDS double*>(base + ly.keyd);
-    DGN_LDS uint64_t* key_j = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.keyj);
     DGN_LDS uint64_t* mask_s = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.mask);
-    DGN_LDS double* sorted_d = reinterpret_cast<DGN_LDS double*>(base + ly.sorted);
     DGN_LDS double* ctab = reinterpret_cast<DGN_LDS double*>(base + ly.ctab);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int lane = lane_id();
+    const int cap = GK ? gk.cap : CAP;
+    using PD = std::conditional_t<GK, double*, DGN_LDS double*>;
+    using PJ = std::conditional_t<GK, uint64_t*, DGN_LDS uint64_t*>;
+    PD kd, sd;
+    PJ kj;
+    // lane-to-lane hand-off through the key rows: LDS (wave order), or global (the agent-scope
+    // fence waits for the wave's stores and invalidates the CU's L1 before the reads)
+    auto key_rows_sync = [&]() __attribute__((always_inline)) {
+        if constexpr (GK) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        else wave_lds_sync();
+    };
+    if constexpr (GK) {
+        double* r = gk.base + ((int64_t)blockIdx.x * kW + w) * (3 * (int64_t)gk.cap + 1);
+        kd = r;
+        kj = reinterpret_cast<uint64_t*>(r + gk.cap);
+        sd = r + 2 * (int64_t)gk.cap;
+    } else {
+        kd = reinterpret_cast<DGN_LDS double*>(base + ly.keyd) + w * CAP;
+        kj = reinterpret_cast<DGN_LDS uint64_t*>(base + ly.keyj) + w * CAP;
+        sd = reinterpret_cast<DGN_LDS double*>(base + ly.sorted) + w * (CAP + 1);
+    }
     // this block's job: row tiles and RBF tiles alternate in the grid (every CU gets both)
     const int64_t both = tl.nrow < tl.nrbf ? tl.nrow : tl.nrbf;
     const int64_t x = blockIdx.x;
@@ -1507,9 +1536,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         }
     __syncthreads();
     EMIT_STAMP(0);
-    DGN_LDS double* kd = key_d + w * CAP;
-    DGN_LDS uint64_t* kj = key_j + w * CAP;
-    DGN_LDS double* sd = sorted_d + w * (CAP + 1);
     for_block_atoms(g, st, 0, g.num_atoms, tile, qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
                                                __attribute__((always_inline)) {
         EMIT_STAMP(1);
@@ -1548,7 +1574,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 const uint64_t bal = ballot(hit);
                 if (hit) {
                     const int slot = m + mask_prefix(bal);
-                    if (slot < CAP) {
+                    if (slot < cap) {
                         kd[slot] = sqrt(d2);  // neighbor_list.cpp:53
                         kj[slot] = pack_jimg(j, na, nb, nc);
                     }
@@ -1558,11 +1584,11 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         EMIT_STAMP(2);
         const int64_t rs0 = row_start[t];
         const int kept = (int)(row_start[t + 1] - rs0);
-        if (m > CAP || kept != (m < K ? m : K)) {
-            if (lane == 0) atomicOr(error_flag, m > CAP ? kGErrCap : kGErrMismatch);
+        if (m > cap || kept != (m < K ? m : K)) {
+            if (lane == 0) atomicOr(error_flag, m > cap ? kGErrCap : kGErrMismatch);
             return;
         }
-        wave_lds_sync();
+        key_rows_sync();
         // 2. rank by (distance, j, image) and place the kept rows
         auto put = [&](int rank, double d, uint64_t key) __attribute__((always_inline)) {
             if (rank >= kept) return;
@@ -1582,15 +1608,17 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 }
             }
         };
-        if (m <= kWave) {
-            if (lane >= m && lane < ((m + 7) & ~7)) kd[lane] = __builtin_inf();  // rank_small reads groups of 8
-            wave_lds_sync();
-            const int r = rank_small(kd, kj, m, lds(claim[w]));
-            if (lane < m) put(r, kd[lane], kj[lane]);
+        if (!GK && m <= kWave) {
+            if constexpr (!GK) {
+                if (lane >= m && lane < ((m + 7) & ~7)) kd[lane] = __builtin_inf();  // rank_small reads groups of 8
+                wave_lds_sync();
+                const int r = rank_small(kd, kj, m, lds(claim[w]));
+                if (lane < m) put(r, kd[lane], kj[lane]);
+            }
         } else {
             rank_large(kd, kj, m, put);
         }
-        wave_lds_sync();
+        key_rows_sync();
         EMIT_STAMP(3);
         if constexpr (!STREAM) {
             // 3. this atom's RBF rows: kept x nbins contiguous values from rs0 * nbins
@@ -1601,7 +1629,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 else
                     write_rbf_flat(reinterpret_cast<double*>(rbf) + rs0 * rs.nbins, total, sd, rs, lane, kWave);
             }
-            wave_lds_sync();
+            key_rows_sync();
         }
     });
     if constexpr (STREAM) {
@@ -1832,50 +1860,57 @@ int graph_emit_cap(uint32_t m, uint64_t kmax) {
     if (m <= 256) return 256;
     if (m <= 512) return 512;
     if (m <= 1024) return 1024;
-    // 1,025..2,048 candidates (cutoffs up to ~20 A at FCC density): the streamed emit only
-    // (max_neighbors <= kStreamMaxK); the per-atom RBF layout would need a sorted-distance buffer
-    // per wave past the LDS
+    // 1,025..2,048 candidates (cutoffs up to ~20 A at FCC density) with max_neighbors <=
+    // kStreamMaxK: the streamed emit (no per-wave sorted-distance buffer) still fits the LDS
     if (m <= 2048 && kmax <= (uint64_t)kStreamMaxK) return 2048;
-    return 0;
+    return kEmitGlobalKeys;  // larger rows: key rows in global memory (emit_key_row_doubles)
 }
+
+int64_t emit_key_row_doubles(uint32_t m) { return 3 * (int64_t)((m + 63) / 64 * 64) + 1; }
+int64_t emit_key_rows_per_chunk() { return kEmitGkChunkBlocks * kW; }
 
 template <int CAP, bool STREAM>
 static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const int32_t* counts,
                           const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
-                          void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
+                          void* rbf, const RbfSpec& rs, uint32_t* error_flag, EmitKeys gk) {
     const int64_t nt = graph_blocks(g.num_atoms, g.qa);
     const int nwm = (stage + 63) / 64;
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
     const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
+    const int fused = STREAM && rs.dtype != 0 && rbf ? 1 : 0;
     auto go = [&](EmitTiles tl) {
         const int64_t blocks = tl.nrow + tl.nrbf;
         if (blocks > 0)
             hipLaunchKernelGGL((graph_emit_kernel<CAP, STREAM>), dim3((unsigned)blocks), dim3(kGraphBlock),
                                (size_t)ly.total, s, g, stage, nwm, counts, block_offsets, row_ptr, col, dist, disp, rbf,
-                               rs, error_flag, tl);
+                               rs, error_flag, tl, gk);
     };
-    if (!STREAM || rs.dtype == 0 || !rbf) {
-        go({0, nt, 0, 0, 0});
+    if (CAP == 0) {
+        // global key rows: one row per wave of a chunk of kEmitGkChunkBlocks tiles, launched in turn
+        for (int64_t t0 = 0; t0 < nt; t0 += kEmitGkChunkBlocks)
+            go({t0, std::min<int64_t>(kEmitGkChunkBlocks, nt - t0), 0, 0, fused});
         return;
     }
     // one launch, each block writes its rows, then its tile's RBF (round 3 A/B: all rows then all
     // RBF in two launches, and a chunk pipeline overlapping rows of chunk i with the RBF of chunk
     // i - 1, were both slower: RBF-only blocks stream at ~4 TB/s and take slots from row blocks)
-    go({0, nt, 0, 0, 1});
+    go({0, nt, 0, 0, fused});
 }
 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
-                             double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag) {
+                             double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag, double* key_rows,
+                             uint32_t max_candidates) {
     const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
     const bool stream = g.kmax <= (uint64_t)kStreamMaxK;
+    EmitKeys gk{nullptr, 0};
 #define DGN_EMIT(C)                                                                                              \
     case C:                                                                                                      \
         if (stream) launch_emit_t<C, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, \
-                                           error_flag);                                                          \
+                                           error_flag, gk);                                                      \
         else launch_emit_t<C, false>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,      \
-                                     error_flag);                                                                \
+                                     error_flag, gk);                                                            \
         break;
     switch (cap) {
         DGN_EMIT(64)
@@ -1885,7 +1920,16 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
         DGN_EMIT(1024)
         case 2048:  // streamed emit only (graph_emit_cap)
             if (!stream) return hipErrorInvalidValue;
-            launch_emit_t<2048, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag);
+            launch_emit_t<2048, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, error_flag,
+                                      gk);
+            break;
+        case kEmitGlobalKeys:
+            if (!key_rows) return hipErrorInvalidValue;
+            gk = {key_rows, (int32_t)((emit_key_row_doubles(max_candidates) - 1) / 3)};
+            if (stream) launch_emit_t<0, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,
+                                               error_flag, gk);
+            else launch_emit_t<0, false>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,
+                                         error_flag, gk);
             break;
         default:
             return hipErrorInvalidValue;

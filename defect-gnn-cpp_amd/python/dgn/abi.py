@@ -25,7 +25,7 @@ EXPORTS = [
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug", "dgn_debug_retry_count",
 ]
-DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_WIDE_WG = 1, 2, 3, 4, 5
+DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2 = 1, 2, 3, 4, 6
 
 
 class DgnError(RuntimeError):
@@ -212,7 +212,8 @@ class Context:
         self._check(lib().dgn_ctx_set_stream(self.h, stream_handle), "set_stream")
 
     def set_debug(self, knob: int, value: int):
-        """Debug / A-B knob (DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_WIDE_WG); tests and tools only."""
+        """Debug / A-B knob (DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP,
+        DEBUG_BIG_LOG2); tests and tools only."""
         self._check(lib().dgn_ctx_set_debug(self.h, knob, value), "set_debug")
 
     def retry_count(self) -> int:

@@ -62,15 +62,16 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  * DGN_DEBUG_WIDE_CAP     > 0: the wide launch's column / pivot / pair tables hold at most this many
  *                        entries (rounded up to a power of two), so ordinary complexes overflow in the
  *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps;
- * DGN_DEBUG_WIDE_WG      default 0: one wave per wide complex (betti_wide); 1 = the experimental
- *                        workgroup-per-complex kernel with the u16 code triangle in LDS for rank-coded
- *                        complexes of 129..362 points (betti_wg; measured slower, off by default). */
+ * DGN_DEBUG_BIG_LOG2     > 0: the capacity-retry layout's first level holds 2^value-entry column /
+ *                        pivot / pair tables and V store (default 2^24), so ordinary complexes outgrow it
+ *                        and are reduced again at the next levels (4x the tables each); 0 = natural. */
 enum {
     DGN_DEBUG_FORCE_RETRY = 1,
     DGN_DEBUG_WIDE_WAVES = 2,
     DGN_DEBUG_WIDE_C16 = 3,
     DGN_DEBUG_WIDE_CAP = 4,
-    DGN_DEBUG_WIDE_WG = 5
+    /* 5: removed (the round-3 workgroup-per-complex kernel) */
+    DGN_DEBUG_BIG_LOG2 = 6
 };
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 /* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */

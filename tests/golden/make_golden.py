@@ -75,10 +75,43 @@ def rc10_fixtures():
     np.savez_compressed(os.path.join(OUT, "rc10.npz"), **out)
 
 
+RC16_ATOMS = (0, 97, 203)
+
+
+def _rc16_one(a):
+    bt = synth.make_batch("fcc", 4, 1)
+    pos, lat = bt["positions"], bt["lattice"][0]
+    nl = O.neighbor_list(lat, pos, 16.0, None)
+    rp = nl["row_ptr"]
+    cloud = np.vstack([pos[a], pos[a] + nl["disp"][rp[a]:rp[a + 1]]])
+    r = O.ref_persistence(O.local_distances(cloud), cloud.shape[0], np.float32(16.0))
+    return a, cloud, r
+
+
+def rc16_fixtures():
+    """(v) Past the 1,024-point envelope of round 3: FCC-256 structure 0 at r_cutoff = 16
+    (~1,370-point complexes, the HUGE wide instantiation), three atoms' clouds (the oracle's
+    NeighborList(16, inf), betti_features.cpp:67-73) and their verbatim-Ripser pairs. ~15 min of
+    CPU per atom: one process per atom. Written to rc16.npz."""
+    from multiprocessing import Pool
+    out = {}
+    with Pool(len(RC16_ATOMS)) as pool:
+        for a, cloud, r in pool.imap_unordered(_rc16_one, RC16_ATOMS):
+            out[f"{a}/cloud"] = cloud
+            for d in ("dim0", "dim1", "dim2"):
+                out[f"{a}/{d}"] = r[d]
+            out[f"{a}/n_inf0"] = np.int32(r["n_inf0"])
+            print("rc16 atom", a, cloud.shape[0], "points", [len(r[d]) for d in ("dim0", "dim1", "dim2")], flush=True)
+    np.savez_compressed(os.path.join(OUT, "rc16.npz"), **out)
+
+
 def main():
     assert O.ref_available(), "build oracle/_ref first (make -C oracle)"
     if sys.argv[1:] == ["rc10"]:
         rc10_fixtures()
+        return
+    if sys.argv[1:] == ["rc16"]:
+        rc16_fixtures()
         return
     # (i) POSCARs: inputs + CSR at rc=5, K=12/20, RBF (rc=5, dr=0.1) of 1 / 741, Betti at rc=5 of all
     poscar = {}

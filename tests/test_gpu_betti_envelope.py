@@ -1,14 +1,15 @@
 """Envelope of the Betti reduction vs the reference's verbatim vendored Ripser (oracle/_ref), which
 has no workspace caps (third_party/ripser/ripser.cpp:514-1269): complexes whose reduction outgrows
 a kernel's per-wave workspace (cliques: every pairwise distance <= threshold) must be reduced again
-by the capacity-retry launch (betti_wide_kernel, big layout) instead of failing. The big layout has
-caps too (2^24 columns / pivots / pairs / V-store words, betti_wide.hip betti_wide_layout): a
-complex beyond those (e.g. a dense clique above ~465 points, C(n, 3) > 2^24) still returns
-DGN_ERR_CAPACITY; the cases here stay inside them. Counts and (birth, death) pairs bit-exact,
-compared as sorted multisets."""
+by the capacity-retry launch (betti_wide_kernel, big layout) instead of failing; a complex that
+outgrows the big layout's tables is listed again and reduced with 4x the tables, up to 2^30
+entries (betti_wide_layout grow levels). Complexes of up to 2,048 points (the HUGE instantiation).
+Counts and (birth, death) pairs bit-exact, compared as sorted multisets."""
+import os
 
 import numpy as np
 import pytest
+from conftest import GOLDEN
 
 import dgn
 import oracle_py as O
@@ -194,17 +195,93 @@ def test_wide_in_kernel_overflow_retry(ctx):
     assert kt == 0, kt
 
 
-def test_above_1024_points_fails_loudly(ctx):
+def test_capacity_retry_grow_levels(ctx):
+    """A complex that outgrows the capacity-retry layout is listed again and reduced with 4x the
+    tables (betti_wide_layout grow levels; the reference's Ripser has no caps). With the first
+    level shrunk to 256-entry tables (DGN_DEBUG_BIG_LOG2 = 8, a test knob) and every complex
+    routed to the retry launch (DGN_DEBUG_FORCE_RETRY), 65..200-point complexes need the later
+    levels (more than one retry launch); against verbatim Ripser."""
+    rng = np.random.default_rng(67)
+    sizes = [200, 150, 90, 30]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.uniform(0, 6.0, size=(n, 3))
+    npts = np.array(sizes, dtype=np.int32)
+    ctx.set_debug(dgn.abi.DEBUG_BIG_LOG2, 8)
+    ctx.set_debug(dgn.abi.DEBUG_FORCE_RETRY, 1)
+    ctx.enable_timing(True)
+    ctx.reset_timing()
+    try:
+        kt = _check(ctx, clouds, npts, 2.0, 4096)
+        launches = ctx.kernel_times().get("betti_retry", {}).get("launches", 0)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_FORCE_RETRY, 0)
+        ctx.set_debug(dgn.abi.DEBUG_BIG_LOG2, 0)
+        ctx.enable_timing(False)
+    assert kt == len(sizes), kt  # each complex reduced once, at the level it fits
+    assert launches >= 2, launches
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
+def test_cloud_above_1024_points(ctx):
+    """Complexes of 1,025..2,048 points: the HUGE instantiation (11-bit vertices, 64-bit packed
+    triangles, the adjacency bitsets in the wave's scratch); 1,900-, 1,300- and 1,030-point clouds
+    plus a small one in the same batch, against verbatim Ripser."""
+    rng = np.random.default_rng(45)
+    sizes = [1900, 1300, 1030, 80]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.uniform(0, 9.0 * (n / 700) ** (1 / 3), size=(n, 3))
+    clouds[1, 40] = clouds[1, 7]  # a duplicate point
+    kt = _check(ctx, clouds, np.array(sizes, dtype=np.int32), 1.6, 1 << 14)
+    assert kt >= 1, kt
+
+
+def test_fcc256_cutoff_16A_every_dim(ctx):
+    """The reference's Betti path at r_cutoff = 16 (betti_features.cpp:67-73, 103-119): FCC-256
+    local complexes of ~1,370 points. Three atoms' clouds (the oracle's NeighborList(16, inf)) and
+    their verbatim-Ripser pairs are committed fixtures (tests/golden/rc16.npz, make_golden.py rc16;
+    ~15 min of Ripser per atom); pairs and counts bit-exact."""
+    fx = np.load(os.path.join(GOLDEN, "rc16.npz"))
+    atoms = sorted({int(k.split("/")[0]) for k in fx.files})
+    clouds_l = [fx[f"{a}/cloud"] for a in atoms]
+    npts = np.array([c.shape[0] for c in clouds_l], np.int32)
+    assert npts.min() > 1024
+    clouds = np.zeros((len(atoms), npts.max(), 3))
+    for c, cl in enumerate(clouds_l):
+        clouds[c, :cl.shape[0]] = cl
+    pairs, counts = ctx.host_persistence(clouds, npts, 16.0, cap=1 << 12)
+    for c, a in enumerate(atoms):
+        got = {"dim0": pairs[c, 0, :counts[c, 0]], "dim1": pairs[c, 1, :counts[c, 2]], "dim2": pairs[c, 2, :counts[c, 3]]}
+        for d in got:
+            assert np.array_equal(np.array(sorted(map(tuple, got[d]))).reshape(-1, 2), fx[f"{a}/{d}"].reshape(-1, 2)), (a, d)
+        assert counts[c, 1] == fx[f"{a}/n_inf0"]
+
+
+def test_fcc256_cutoff_16A_structure(ctx):
+    """compute_structure_betti_features at r_cutoff = 16 for every atom of FCC-256 structure 0
+    through the whole device path (NeighborList(16, inf) search of up to 2,048 candidates, the
+    MFMA distance pass, rank codes, the HUGE wide launch); the fixture atoms' counts equal the
+    verbatim-Ripser pair counts."""
+    fx = np.load(os.path.join(GOLDEN, "rc16.npz"))
+    f, c = ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 16.0)
+    assert not np.isnan(f).any() and (c >= 0).all()
+    for a in sorted({int(k.split("/")[0]) for k in fx.files}):
+        assert c[a].tolist() == [len(fx[f"{a}/dim0"]), int(fx[f"{a}/n_inf0"]), len(fx[f"{a}/dim1"]),
+                                 len(fx[f"{a}/dim2"])], a
+
+
+def test_above_2048_points_fails_loudly(ctx):
     # outside the envelope (DESIGN.md §8): an explicit DGN_ERR_UNSUPPORTED, never a silent or
-    # truncated result -- a caller-given 1,100-point cloud, and FCC-256 at 15.5 A (≈ 1,300-point
+    # truncated result -- a caller-given 2,100-point cloud, and FCC-256 at 21 A (~3,100-point
     # local complexes, the count pass finds them before any Betti launch)
     rng = np.random.default_rng(5)
-    cloud = rng.uniform(0.0, 100.0, size=(1, 1100, 3))
+    cloud = rng.uniform(0.0, 100.0, size=(1, 2100, 3))
     with pytest.raises(dgn.DgnError) as e:
-        ctx.host_persistence(cloud, np.array([1100], np.int32), 1.0)
+        ctx.host_persistence(cloud, np.array([2100], np.int32), 1.0)
     assert e.value.status == 5
     with pytest.raises(dgn.DgnError) as e:
-        ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 15.5)
+        ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 21.0)
     assert e.value.status == 5
     # the context stays usable
     f, c = ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 5.0)

@@ -20,9 +20,6 @@ def _ref(low, n, thr):
     return O.ref_persistence(low, n, thr) if O.ref_available() else O.persistence(low, n, thr)
 
 
-WG_DEFAULT = 0  # the library's default for DGN_DEBUG_WIDE_WG (0: one wave per complex)
-
-
 def _check_clouds(ctx, clouds, npts, thr, cap):
     pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=cap)
     bad = []
@@ -71,23 +68,17 @@ def _rc10_inputs(name):
     return dgn.synth_batch("fcc", 4, 1)
 
 
-@pytest.mark.parametrize("wg", [0, 1])
 @pytest.mark.parametrize("name", ["741", "fcc256_0"])
-def test_default_cutoff_10A_every_atom(ctx, name, wg):
+def test_default_cutoff_10A_every_atom(ctx, name):
     """compute_structure_betti_features at the reference's default r_cutoff = 10
     (preprocess_betti.cpp:117; betti_features.cpp:103-119) for EVERY atom of 741.vasp (120 atoms,
-    ~300-point complexes) and of FCC-256 structure 0 (256 atoms, ~340 points), with the one-wave
-    (wg 0, the default) and the workgroup-per-complex (wg 1) wide kernels, against the
+    ~300-point complexes) and of FCC-256 structure 0 (256 atoms, ~340 points) against the
     verbatim-Ripser fixtures: counts bit-exact, statistics within 1e-6."""
     fx = np.load(os.path.join(GOLDEN, "rc10.npz"))
     batch = _rc10_inputs(name)
     if name == "fcc256_0":
         assert np.array_equal(batch["positions"], fx["fcc256_0/positions"])  # generator bit-identity
-    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, wg)
-    try:
-        f, c = ctx.host_betti(batch, 10.0)
-    finally:
-        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, WG_DEFAULT)
+    f, c = ctx.host_betti(batch, 10.0)
     fo, co = fx[f"{name}/features"], fx[f"{name}/counts"]
     assert f.shape == fo.shape and not np.isnan(f).any()
     bad = np.nonzero((c != co).any(axis=1))[0]
@@ -127,30 +118,3 @@ def test_f32_fallback_matches_rank_codes(ctx):
         for d, col in ((0, 0), (1, 2), (2, 3)):
             n = k16[c, col]
             assert np.array_equal(p32[c, d, :n], p16[c, d, :n]), (c, d)
-
-
-def test_workgroup_kernel_matches_wave_kernel(ctx):
-    """The workgroup-per-complex kernel (DGN_DEBUG_WIDE_WG = 1, off by default: rank-coded
-    129..362-point complexes, distances in LDS) and the default one-wave-per-complex kernel give
-    the same pairs and counts; both against verbatim Ripser (ripser.cpp:514-1269)."""
-    rng = np.random.default_rng(47)
-    sizes = [340, 200, 131, 90, 362]
-    clouds = np.zeros((len(sizes), max(sizes), 3))
-    for c, n in enumerate(sizes):
-        clouds[c, :n] = rng.uniform(0, 6.5, size=(n, 3))
-    clouds[1, 100:120] = clouds[1, 0:20]  # exact duplicate points: zero distances and ties
-    npts = np.array(sizes, dtype=np.int32)
-    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 1)
-    try:
-        _check_clouds(ctx, clouds, npts, 1.8, 16384)
-        pwg, kwg = ctx.host_persistence(clouds, npts, 1.8, cap=16384)
-        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, 0)
-        pw, kw = ctx.host_persistence(clouds, npts, 1.8, cap=16384)
-    finally:
-        ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, WG_DEFAULT)
-    assert np.array_equal(kw, kwg)
-    for c in range(len(sizes)):
-        for d, col in ((0, 0), (1, 2), (2, 3)):
-            n = kwg[c, col]
-            a, b = pw[c, d, :n], pwg[c, d, :n]
-            assert np.array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])]), (c, d)

@@ -172,9 +172,8 @@ def test_device_count_emit_full_shard(ctx):
 
 
 def test_fcc256_cutoff_17A_above_1024_candidates(ctx):
-    """NeighborList(rc = 17, K = 20): ~1,200 candidates per atom (the 2,048-candidate streamed
-    emit), CSR bit-exact; the same cutoff without a neighbour cap (per-atom RBF rows) is outside the
-    envelope and fails loudly."""
+    """NeighborList(rc = 17, K = 20): ~1,650 candidates per atom (the 2,048-candidate streamed
+    emit), CSR bit-exact."""
     batch = dgn.synth_batch("fcc", 4, 1)
     p = abi.graph_params(r_cutoff=17.0, max_neighbors=20, rbf_cutoff=17.0, rbf_dr=0.1, write_displacement=True)
     g = ctx.host_graph(batch, p)
@@ -184,11 +183,25 @@ def test_fcc256_cutoff_17A_above_1024_candidates(ctx):
     assert np.array_equal(g["dist"], dist)
     assert np.array_equal(g["disp"], disp)
     check_rbf(g["rbf"], dist, 17.0, 0.1)
-    # without a neighbour cap the per-atom sorted-distance buffer holds at most 1,024 candidates:
-    # a loud DGN_ERR_UNSUPPORTED (status 5), not any other failure
-    with pytest.raises(dgn.DgnError) as e:
-        ctx.host_graph(batch, abi.graph_params(r_cutoff=17.0, max_neighbors=None, rbf_cutoff=5.0, rbf_dr=0.1))
-    assert e.value.status == 5
+
+
+@pytest.mark.parametrize("rc,k", [(17.0, None), (20.0, 20), (20.0, None)])
+def test_fcc256_large_rows_global_keys(ctx, rc, k):
+    """Rows past the LDS hit lists (more than 2,048 candidates, or more than 1,024 without a
+    neighbour cap; neighbor_list.cpp:27-66 has no cap): the emit keeps each wave's hit list, keys
+    and sorted distances in HBM (kEmitGlobalKeys). FCC-256 at 17 A (~1,650 candidates, K = inf)
+    and 20 A (~2,700), CSR, distances and displacements bit-exact vs the oracle, RBF within 1e-13."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    p = abi.graph_params(r_cutoff=rc, max_neighbors=k, rbf_cutoff=5.0, rbf_dr=0.1, write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, rc, k)
+    if k is None:
+        assert np.diff(rp).max() > (2048 if rc == 20.0 else 1024)
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
+    check_rbf(g["rbf"], dist, 5.0, 0.1)
 
 
 @pytest.mark.parametrize("k", [20, None])
