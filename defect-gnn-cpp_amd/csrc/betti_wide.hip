@@ -55,6 +55,8 @@ __device__ __forceinline__ uint32_t rlw(uint32_t x, int l) { return (uint32_t)__
 __device__ __forceinline__ uint64_t rlw64(uint64_t x, int l) {
     return ((uint64_t)rlw((uint32_t)(x >> 32), l) << 32) | rlw((uint32_t)x, l);
 }
+// lanes 0 .. m - 1 (m in 0..64)
+__device__ __forceinline__ uint64_t lanes_below_w(int m) { return m >= 64 ? ~0ull : (1ull << m) - 1ull; }
 __device__ __forceinline__ uint32_t uniw(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uniw64(uint64_t x) {
     return ((uint64_t)uniw((uint32_t)(x >> 32)) << 32) | uniw((uint32_t)x);
@@ -128,6 +130,10 @@ struct WideCx {
     uint32_t err;
     int n_d0, n_inf0, n_p1, n_p2;
     const uint32_t* vals = nullptr;  // CODED: the complex's sorted f32 distances (code -> value)
+    // the working column's V list: in registers (lane i holds entry i) while it has <= 64 entries,
+    // else (vspill, uniform) in scratch (vlist)
+    PT vreg = 0;
+    bool vspill = false;
 #ifdef DGN_PHASE_TIMING
     uint64_t dg_searches = 0, dg_floor_iters = 0;  // diagnostics: pivot searches and their floor rounds
 #endif
@@ -734,7 +740,8 @@ struct WideCx {
         return kNoMetaW;
     }
 
-    // ---- the working column's V list (scratch: vlist[0..v), packed simplices, no small cap) ----
+    // ---- the working column's V list: registers up to 64 entries, then scratch (vlist[0..v),
+    // packed simplices, no small cap) ----
     __device__ int v_find(PT x, int v) const {
         const int lane = lane_id();
         const PT* VL = sp<PT>(ly.vlist);
@@ -746,17 +753,38 @@ struct WideCx {
         return -1;
     }
     __device__ bool v_toggle(PT x, int& v) {  // V ^= {x}; false on overflow
+        const int lane = lane_id();
+        if (!vspill) {
+            // register list: no memory round trip (find by ballot, remove by moving the last entry)
+            const uint64_t hit = ballot(vreg == x) & lanes_below_w(v);
+            if (hit) {
+                const int pos = __ffsll((unsigned long long)hit) - 1;
+                const PT last = rlp(vreg, v - 1);
+                if (lane == pos) vreg = last;
+                v = v - 1;
+                return true;
+            }
+            if (v < kWave) {
+                if (lane == v) vreg = x;
+                v = v + 1;
+                return true;
+            }
+            // a 65th entry: the list moves to scratch
+            sp<PT>(ly.vlist)[lane] = vreg;
+            vspill = true;
+            wave_scratch_sync();
+        }
         PT* VL = sp<PT>(ly.vlist);
         const int pos = v_find(x, v);
         if (pos >= 0) {
             if (pos != v - 1) {
                 const PT last = unip(VL[v - 1]);
-                if (lane_id() == 0) VL[pos] = last;
+                if (lane == 0) VL[pos] = last;
             }
             v = v - 1;
         } else {
             if (v >= ly.vl_cap) return false;
-            if (lane_id() == 0) VL[v] = x;
+            if (lane == 0) VL[v] = x;
             v = v + 1;
         }
         wave_scratch_sync();  // the list (scratch) is read by every lane next
@@ -772,7 +800,7 @@ struct WideCx {
         const PT* VL = sp<PT>(ly.vlist);
         // V entries and their diameters live in registers (lane i: entry base + i), read back with
         // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
-        const PT vl0 = k < v ? VL[k] : PT(0);
+        const PT vl0 = k < v ? (vspill ? VL[k] : vreg) : PT(0);
         const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
 #ifdef DGN_PHASE_TIMING
         ++dg_searches;
@@ -899,6 +927,7 @@ struct WideCx {
             uint64_t meta = lookup(dim, tau, tv, app);
             WSUB(1);
             int v = 0;  // 0 = lazy: V == {this column}
+            vspill = false;
             if (meta != kNoMetaW || app != kNoneP) {
                 v_toggle(cp, v);
                 int64_t guard = 0;
@@ -951,8 +980,12 @@ struct WideCx {
                     err |= kER;
                     break;
                 }
-                const PT* VL = sp<PT>(ly.vlist);
-                for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
+                if (vspill) {
+                    const PT* VL = sp<PT>(ly.vlist);
+                    for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
+                } else if (lane < v) {
+                    vstore[vused + lane] = vreg;
+                }
                 wave_scratch_sync();
                 m = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;

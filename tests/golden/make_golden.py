@@ -90,19 +90,18 @@ def _rc16_one(a):
 
 def rc16_fixtures():
     """(v) Past the 1,024-point envelope of round 3: FCC-256 structure 0 at r_cutoff = 16
-    (~1,370-point complexes, the HUGE wide instantiation), three atoms' clouds (the oracle's
-    NeighborList(16, inf), betti_features.cpp:67-73) and their verbatim-Ripser pairs. ~15 min of
-    CPU per atom: one process per atom. Written to rc16.npz."""
-    from multiprocessing import Pool
+    (~1,400-point complexes, the HUGE wide instantiation), three atoms' clouds (the oracle's
+    NeighborList(16, inf), betti_features.cpp:67-73) and their verbatim-Ripser pairs. Ripser needs
+    ~15 min and ~34 GB per atom here: one atom at a time, rc16.npz rewritten after each."""
     out = {}
-    with Pool(len(RC16_ATOMS)) as pool:
-        for a, cloud, r in pool.imap_unordered(_rc16_one, RC16_ATOMS):
-            out[f"{a}/cloud"] = cloud
-            for d in ("dim0", "dim1", "dim2"):
-                out[f"{a}/{d}"] = r[d]
-            out[f"{a}/n_inf0"] = np.int32(r["n_inf0"])
-            print("rc16 atom", a, cloud.shape[0], "points", [len(r[d]) for d in ("dim0", "dim1", "dim2")], flush=True)
-    np.savez_compressed(os.path.join(OUT, "rc16.npz"), **out)
+    for a in RC16_ATOMS:
+        a, cloud, r = _rc16_one(a)
+        out[f"{a}/cloud"] = cloud
+        for d in ("dim0", "dim1", "dim2"):
+            out[f"{a}/{d}"] = r[d]
+        out[f"{a}/n_inf0"] = np.int32(r["n_inf0"])
+        print("rc16 atom", a, cloud.shape[0], "points", [len(r[d]) for d in ("dim0", "dim1", "dim2")], flush=True)
+        np.savez_compressed(os.path.join(OUT, "rc16.npz"), **out)
 
 
 def main():

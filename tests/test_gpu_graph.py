@@ -190,9 +190,10 @@ def test_fcc256_large_rows_global_keys(ctx, rc, k):
     """Rows past the LDS hit lists (more than 2,048 candidates, or more than 1,024 without a
     neighbour cap; neighbor_list.cpp:27-66 has no cap): the emit keeps each wave's hit list, keys
     and sorted distances in HBM (kEmitGlobalKeys). FCC-256 at 17 A (~1,650 candidates, K = inf)
-    and 20 A (~2,700), CSR, distances and displacements bit-exact vs the oracle, RBF within 1e-13."""
+    and 20 A (~2,700), CSR, distances and displacements bit-exact vs the oracle, f32 RBF (0.5 A
+    bins to the cutoff) within 1e-6."""
     batch = dgn.synth_batch("fcc", 4, 1)
-    p = abi.graph_params(r_cutoff=rc, max_neighbors=k, rbf_cutoff=5.0, rbf_dr=0.1, write_displacement=True)
+    p = abi.graph_params(r_cutoff=rc, max_neighbors=k, rbf_cutoff=rc, rbf_dr=0.5, write_displacement=True)
     g = ctx.host_graph(batch, p)
     rp, col, dist, disp = oracle_batch_csr(batch, rc, k)
     if k is None:
@@ -201,7 +202,7 @@ def test_fcc256_large_rows_global_keys(ctx, rc, k):
     assert np.array_equal(g["col"], col)
     assert np.array_equal(g["dist"], dist)
     assert np.array_equal(g["disp"], disp)
-    check_rbf(g["rbf"], dist, 5.0, 0.1)
+    check_rbf(g["rbf"], dist, rc, 0.5)
 
 
 @pytest.mark.parametrize("k", [20, None])
