@@ -131,7 +131,9 @@ struct WideCx {
     int n_d0, n_inf0, n_p1, n_p2;
     const uint32_t* vals = nullptr;  // CODED: the complex's sorted f32 distances (code -> value)
     // the working column's V list: in registers (lane i holds entry i) while it has <= 64 entries,
-    // else (vspill, uniform) in scratch (vlist)
+    // else (vspill, uniform) in scratch (vlist); scratch only for the 8-word instantiation (its
+    // registers are spent: the register list there spilled 150 VGPRs)
+    static constexpr bool VREG = KW <= 6 || KW > 8;
     PT vreg = 0;
     bool vspill = false;
 #ifdef DGN_PHASE_TIMING
@@ -147,6 +149,21 @@ struct WideCx {
         return sp<uint32_t>(ly.D)[(int64_t)i * n + j];
     }
     __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
+    // d(a, x) for a wave-uniform row a: scalar row base + 32-bit lane offset
+    __device__ uint32_t drow(int a, uint32_t x) const {
+        const uint32_t ra = (uint32_t)a * (uint32_t)n;
+        if (MODE == kC16) return at(sp<uint16_t>(ly.D) + ra, x);
+        return at(sp<uint32_t>(ly.D) + ra, x);
+    }
+    // u16 codes (n <= 362, 9-bit vertices): the pivot search compares cofacets by the packed-tuple
+    // key (code << 36) | ~tuple, order-isomorphic to (code << 32) | ~index (a tuple packed
+    // descending compares as its colex index), so a candidate costs no binomials; the winner's
+    // index is computed once
+    static constexpr bool PACKKEY = MODE == kC16;
+    static constexpr int PKS = 36;
+    __device__ static uint64_t pkey(uint32_t dc, uint64_t tuple) {
+        return ((uint64_t)dc << PKS) | (~tuple & ((1ull << PKS) - 1));
+    }
     __device__ bool is_tree(int i, int j) const { return par[i] == j || par[j] == i; }
     __device__ uint32_t sdiam(int dim, uint64_t p) const {  // dim 1: edge, dim 2: triangle
         if (dim == 1) return d(pv(p, 1), pv(p, 0));
@@ -754,7 +771,7 @@ struct WideCx {
     }
     __device__ bool v_toggle(PT x, int& v) {  // V ^= {x}; false on overflow
         const int lane = lane_id();
-        if (!vspill) {
+        if (VREG && !vspill) {
             // register list: no memory round trip (find by ballot, remove by moving the last entry)
             const uint64_t hit = ballot(vreg == x) & lanes_below_w(v);
             if (hit) {
@@ -794,13 +811,14 @@ struct WideCx {
     // Pivot of sum(delta s, s in V) above `floor` (the previous pivot): lane k evaluates the
     // cofacets s u {x}, x = 64 t + k; a cofacet arises once per facet in V; the multiplicity of
     // the minimum is summed over lanes (a lane can meet it from several words). Even: raise the
-    // floor and repeat. Returns kInf for the zero column; tv = packed pivot.
+    // floor and repeat. Returns kInf for the zero column; tv = packed pivot (in: the floor's).
     __device__ uint64_t pivot_of_V(int dim, int v, uint64_t floor, uint64_t& tv) {
         const int k = lane_id();
+        if constexpr (PACKKEY) floor = pkey(kdiam(floor), tv);  // tv: the floor's packed tuple
         const PT* VL = sp<PT>(ly.vlist);
         // V entries and their diameters live in registers (lane i: entry base + i), read back with
         // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
-        const PT vl0 = k < v ? (vspill ? VL[k] : vreg) : PT(0);
+        const PT vl0 = k < v ? ((VREG && !vspill) ? vreg : VL[k]) : PT(0);
         const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
 #ifdef DGN_PHASE_TIMING
         ++dg_searches;
@@ -820,9 +838,15 @@ struct WideCx {
 #pragma unroll
                 for (int t = 0; t < KW; ++t) {
                     const int x = min(64 * t + k, n - 1);
-                    da[t] = d(a, x);
-                    db[t] = d(b, x);
-                    dc[t] = dim == 2 ? d(c, x) : 0u;
+                    if constexpr (PACKKEY) {
+                        da[t] = drow(a, (uint32_t)x);
+                        db[t] = drow(b, (uint32_t)x);
+                        dc[t] = dim == 2 ? drow(c, (uint32_t)x) : 0u;
+                    } else {
+                        da[t] = d(a, x);
+                        db[t] = d(b, x);
+                        dc[t] = dim == 2 ? d(c, x) : 0u;
+                    }
                 }
 #pragma unroll
                 for (int t = 0; t < KW; ++t) {
@@ -832,7 +856,7 @@ struct WideCx {
                     const int x = 64 * t + k;
                     const uint32_t dd = max(max(ds, dc[t]), max(da[t], db[t]));
                     const uint64_t p = pinsert(dim + 1, s, x);
-                    const uint64_t kk = wkey(dd, pidx(dim + 2, p));
+                    const uint64_t kk = PACKKEY ? pkey(dd, p) : wkey(dd, pidx(dim + 2, p));
                     if (((am >> k) & 1ull) && kk > floor) {  // x is a common neighbour (so x < n)
                         if (kk < lmin) {
                             lmin = kk;
@@ -873,6 +897,7 @@ struct WideCx {
             if (cnt & 1) {
                 const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
                 tv = rlw64(lp, l);
+                if constexpr (PACKKEY) return wkey((uint32_t)(m >> PKS), pidx(dim + 2, tv));
                 return m;
             }
             floor = m;
@@ -927,7 +952,7 @@ struct WideCx {
             uint64_t meta = lookup(dim, tau, tv, app);
             WSUB(1);
             int v = 0;  // 0 = lazy: V == {this column}
-            vspill = false;
+            vspill = !VREG;
             if (meta != kNoMetaW || app != kNoneP) {
                 v_toggle(cp, v);
                 int64_t guard = 0;
@@ -980,7 +1005,7 @@ struct WideCx {
                     err |= kER;
                     break;
                 }
-                if (vspill) {
+                if (!VREG || vspill) {
                     const PT* VL = sp<PT>(ly.vlist);
                     for (int t = lane; t < v; t += kWave) vstore[vused + t] = VL[t];
                 } else if (lane < v) {

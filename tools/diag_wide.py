@@ -13,8 +13,6 @@ import dgn  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 ctx = dgn.Context(0)
-if os.environ.get("DGN_WIDE_WG"):
-    ctx.set_debug(dgn.abi.DEBUG_WIDE_WG, int(os.environ["DGN_WIDE_WG"]))
 batch = dgn.synth_batch("fcc", 4, B)
 A = batch["positions"].shape[0]
 t0 = time.perf_counter()
