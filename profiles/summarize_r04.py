@@ -1,0 +1,172 @@
+"""Round-4 evidence beside parse_profiles.py (bench trace + path PMC): folds the rest of
+profiles/collect_r04.sh's output into committed summaries.
+    python profiles/summarize_r04.py [gpurun_out/prof_r04]
+Writes (profiles/):
+  r04_narrow44_sq.txt / r04_narrow44_mem.txt   per-kernel PMC of the narrow Betti kernels
+  r04_narrow_before_after.json                 betti_kernel<44> counters, round 3 -> round 4
+  r04_mfma.json                                distance kernel MFMA counters + derived rates
+  r04_rc10_wide.json                           the 10 A wide kernel: time, HBM bytes and SQ mix per complex
+  r04_side_graph.json                          per-kernel medians of BASELINE configs 2 and 5 (f32 / f64 RBF)
+SQ cycle counters (SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_*) are in quad-cycles
+(MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"); instruction counters are per wave instruction.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+D = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(HERE), "gpurun_out", "prof_r04")
+FP64_MFMA_PEAK_TFS = 78.6
+CLOCK_GHZ = 2.4
+SIMDS = 1024
+
+
+def rows(sub):
+    out = []
+    for p in sorted(glob.glob(os.path.join(D, sub, "**", "*counter_collection.csv"), recursive=True)):
+        with open(p) as f:
+            out += list(csv.DictReader(f))
+    return out
+
+
+def per_kernel(sub, want=None):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in rows(sub):
+        name = r["Kernel_Name"]
+        name = name[:name.rfind("(")] if name.endswith(")") else name
+        if want and want not in name:
+            continue
+        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def pmc_text(sub, path):
+    with open(path, "w") as f:
+        for k, cs in sorted(per_kernel(sub).items()):
+            if "betti_kernel" not in k:
+                continue
+            f.write(f"{k}\n")
+            for c, v in sorted(cs.items()):
+                f.write(f"    {c:32s} {v:18.1f}\n")
+
+
+def parse_txt(path):
+    out, cur = {}, None
+    for line in open(path):
+        if not line.startswith(" "):
+            cur = line.strip()
+            out[cur] = {}
+        elif cur:
+            p = line.split()
+            out[cur][p[0]] = float(p[1])
+    return out
+
+
+def main():
+    pmc_text("narrow_sq1", os.path.join(HERE, "r04_narrow44_sq.txt"))
+    with open(os.path.join(HERE, "r04_narrow44_sq.txt"), "a") as f:
+        for k, cs in sorted(per_kernel("narrow_sq2").items()):
+            if "betti_kernel" in k:
+                f.write(f"{k} (pass 2)\n")
+                for c, v in sorted(cs.items()):
+                    f.write(f"    {c:32s} {v:18.1f}\n")
+    pmc_text("narrow_mem", os.path.join(HERE, "r04_narrow44_mem.txt"))
+    k44 = "void dgn::betti_kernel<44>"
+    after = {}
+    for sub in ("narrow_sq1", "narrow_sq2", "narrow_mem"):
+        after.update(per_kernel(sub).get(k44, {}))
+    before = {}
+    for f in ("r03_narrow44_sq.txt", "r03_narrow44_mem.txt"):
+        before.update(parse_txt(os.path.join(HERE, f)).get(k44, {}))
+    keys = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_VMEM",
+            "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_LDS", "TCP_TCC_WRITE_REQ_sum", "TCP_TCC_READ_REQ_sum",
+            "TCC_EA0_WRREQ_sum", "TCC_EA0_RDREQ_sum")
+    ba = {"workload": "tools/betti_run.py fcc 4 2048 5.0 1 (2,048 FCC-256 structures at 5 A: 524,288 complexes); "
+                      "betti_kernel<44> alone (the <= 44-point main tier)",
+          "counters": {k: {"r03": before.get(k), "r04": after.get(k),
+                           "ratio": round(after[k] / before[k], 3) if before.get(k) and after.get(k) else None}
+                       for k in keys}}
+    if after.get("SQ_INSTS_LDS"):
+        ba["lds_conflict_cycles_per_lds_inst"] = {"r03": round(before["SQ_LDS_BANK_CONFLICT"] / before["SQ_INSTS_LDS"], 3),
+                                                   "r04": round(after["SQ_LDS_BANK_CONFLICT"] / after["SQ_INSTS_LDS"], 3)}
+        ba["lds_conflict_share_of_wave_cycles"] = round(after["SQ_LDS_BANK_CONFLICT"] / (4 * after["SQ_WAVE_CYCLES"]), 4)
+    json.dump(ba, open(os.path.join(HERE, "r04_narrow_before_after.json"), "w"), indent=1)
+
+    # MFMA counters of the distance kernel (betti_dist_search_kernel<64>), durations from the bench trace
+    m = per_kernel("mfma").get("void dgn::betti_dist_search_kernel<64>", {})
+    summ = json.load(open(os.path.join(HERE, "r04_summary.json")))
+    dur = summ["trace_launch_ms"]["betti_dist_search_kernel"]
+    ms = sum(dur) / len(dur)
+    flops_issued = m["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512  # MfmaFlopsF64 (rocprofiler counter_defs.yaml)
+    mf = {"kernel": "betti_dist_search_kernel<64> (config-4 shard: 2,097,152 local complexes of <= 64 points)",
+          "counters_per_launch": m, "avg_launch_ms": round(ms, 4),
+          "mfma_f64_flops_issued_per_launch": flops_issued,
+          "mfma_f64_issued_tflops": round(flops_issued / (ms * 1e-3) / 1e12, 3),
+          "mfma_f64_issued_frac_of_peak": round(flops_issued / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS, 4),
+          "mfma_busy_frac": round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (ms * 1e-3 * CLOCK_GHZ * 1e9 * SIMDS), 4),
+          "useful": summ["trace_bench"]["roofline_mfma"],
+          "note": "each 16x16 tile issues three v_mfma_f64_16x16x4_f64 with one live k each (exact products, the "
+                  "reference's (p0 + p1) + p2 order), so 1/4 of the issued flops are the K = 3 Gram product and the "
+                  "useful 6n^2 per complex is a smaller figure still (padding to 16-row tiles); MfmaFlopsF64 = "
+                  "SQ_INSTS_VALU_MFMA_MOPS_F64 x 512; busy = SQ_VALU_MFMA_BUSY_CYCLES / (launch cycles x 1,024 SIMDs)"}
+    json.dump(mf, open(os.path.join(HERE, "r04_mfma.json"), "w"), indent=1)
+
+    # the 10 A wide kernel (tools/betti_rc10.py 16 1: 4,096 complexes)
+    nc = 4096
+    wide = {}
+    for sub in ("wide_fetch", "wide_write", "wide_sq1", "wide_sq2"):
+        for r in rows(sub):
+            if "betti_wide" in r["Kernel_Name"]:
+                wide[r["Counter_Name"]] = float(r["Counter_Value"])
+    st = {}
+    p = glob.glob(os.path.join(D, "wide_trace", "**", "*kernel_stats.csv"), recursive=True)
+    if p:
+        with open(p[0]) as f:
+            st = {r["Name"][:90]: round(float(r["AverageNs"]) / 1e6, 3) for r in csv.DictReader(f)}
+    rc = {"workload": "tools/betti_rc10.py 16 1: 16 FCC-256 structures at rc 10 (4,096 complexes of ~340 points)",
+          "kernel_ms": st,
+          "per_complex": {k: round(v / nc, 1) for k, v in wide.items()},
+          "hbm_mb_per_complex": {"fetch_x1": round(wide.get("FETCH_SIZE", 0) * 1024 / nc / 1e6, 1),
+                                 "fetch_x2": round(2 * wide.get("FETCH_SIZE", 0) * 1024 / nc / 1e6, 1),
+                                 "write": round(wide.get("WRITE_SIZE", 0) * 1024 / nc / 1e6, 1)},
+          "note": "FETCH_SIZE / WRITE_SIZE in KB; the x2 gfx950 correction is calibrated for 16-B-per-lane streaming "
+                  "reads, these are 2-byte scattered reads (uncalibrated: both readings given)"}
+    if wide.get("SQ_WAVE_CYCLES"):
+        rc["issue_frac"] = round(wide["SQ_ACTIVE_INST_ANY"] / wide["SQ_WAVE_CYCLES"], 3)
+        rc["wait_frac"] = round(wide["SQ_WAIT_ANY"] / wide["SQ_WAVE_CYCLES"], 3)
+    json.dump(rc, open(os.path.join(HERE, "r04_rc10_wide.json"), "w"), indent=1)
+
+    # BASELINE configs 2 and 5 (tools/side_graph.py 20: config2, config5 f32, then f64), per dispatch
+    tr = glob.glob(os.path.join(D, "side", "**", "*kernel_trace.csv"), recursive=True)
+    if tr:
+        rs = sorted(csv.DictReader(open(tr[0])), key=lambda r: int(r["Start_Timestamp"]))
+        acc = collections.defaultdict(list)
+        for r in rs:
+            if "dgn::" not in r["Kernel_Name"]:
+                continue
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dgn::", "")
+            acc[(name, int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        out = {"config2": {"f32": {}, "f64": {}}, "config5": {"f32": {}, "f64": {}}}
+        big = max(g for (_, g) in acc)
+        for (name, grid), v in acc.items():
+            cfg = "config2" if grid == big or (name in ("prep_atoms_kernel",) and grid > 1024) or \
+                (name == "prep_meta_kernel" and grid == 1024) else "config5"
+            h = len(v) // 2
+            for half, vals in (("f32", v[:h]), ("f64", v[h:])):
+                vals = sorted(vals)
+                if vals:
+                    out[cfg][half][name] = round(vals[len(vals) // 2], 2)
+        for cfg in out:
+            for dt in out[cfg]:
+                out[cfg][dt]["path_us"] = round(sum(x for k, x in out[cfg][dt].items() if k != "path_us"), 1)
+        out["note"] = ("median kernel durations (us) per dispatch, rocprofv3 --kernel-trace; config 2 = 1,024 SC-64 cells "
+                       "(grid 2,048 blocks), config 5 = one 4,096-atom SC supercell (1,024 blocks of 4 atoms); "
+                       "graph rc 5, K 20, 50-bin RBF")
+        json.dump(out, open(os.path.join(HERE, "r04_side_graph.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
