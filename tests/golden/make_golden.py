@@ -2,6 +2,7 @@
 
     python tests/golden/make_golden.py          # everything
     python tests/golden/make_golden.py rc10     # only the 10 A fixtures (rc10.npz)
+    python tests/golden/make_golden.py rc16     # only the 16 A fixtures (rc16.npz; ~45 min, ~34 GB)
 
 Inputs: the reference's own POSCAR files (/root/reference/web/public/data/structures/*.vasp,
 parsed here as data) and synthetic SC cells from the bit-reproducible generator.
