@@ -36,3 +36,21 @@ def test_rc10_fixture_inputs_match_generator():
         c = fx[f"{name}/counts"]
         assert c.shape == (n, 4) and fx[f"{name}/features"].shape == (n, 35)
         assert np.all(c[:, 1] == 1) and np.all(c[:, 2] > 0)
+
+
+def test_rc16_fixture_clouds_match_oracle_neighbour_list():
+    """tests/golden/rc16.npz holds three FCC-256 atoms' local clouds at r_cutoff = 16 (centre +
+    NeighborList(16, inf) displacements, betti_features.cpp:67-73) with their verbatim-Ripser pairs:
+    the clouds are the oracle's for the generator's structure 0, so the GPU test feeds the same
+    complexes; each is past the 1,024-point envelope of round 3."""
+    import os
+    import oracle_py as O
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "rc16.npz"))
+    b = synth.make_batch("fcc", 4, 1)
+    nl = O.neighbor_list(b["lattice"][0], b["positions"], 16.0, None)
+    rp = nl["row_ptr"]
+    for a in (0, 97, 203):
+        cloud = np.vstack([b["positions"][a], b["positions"][a] + nl["disp"][rp[a]:rp[a + 1]]])
+        assert np.array_equal(fx[f"{a}/cloud"], cloud)
+        assert cloud.shape[0] > 1024
+        assert len(fx[f"{a}/dim0"]) + int(fx[f"{a}/n_inf0"]) == cloud.shape[0]
