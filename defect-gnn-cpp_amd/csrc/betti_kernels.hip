@@ -762,7 +762,14 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
     if (lane_id() < 32) ph[lane_id()] = 0;
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
-    const int lane = lane_id();
+    // the lane index is re-derived opaquely at every phase (relane): the compiler cannot hoist
+    // lane-derived masks and per-lane addresses out of the complex loop, where they were live
+    // across the whole kernel and spilled (16 VGPRs at the 96-VGPR budget of NP = 44)
+    int lane = lane_id();
+    auto relane = [&]() __attribute__((always_inline)) {
+        lane = lane_id();
+        asm volatile("" : "+v"(lane));
+    };
     // all-ones diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key)
     if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0xFFFFFFFFu);
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
@@ -845,6 +852,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             lds_sync();
             DGN_PHASE(0); DGN_STOP(1)
             // ---- adjacency (sparse_distance_matrix: i != j and d <= thr, ripser.cpp:386-395) ----
+            relane();
             uint64_t myadj = 0;  // this lane's row
             {
                 for (int i = 0; i < n; ++i) {
@@ -859,6 +867,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             cx.n_inf0 = 0;
             cx.n_d0 = 0;
             // ---- dim 0: Prim on F-keys == Kruskal's forest in Ripser order (ripser.cpp:725-762) ----
+            relane();
             // best = the lane's F-minimal edge to the forest (kInf once the lane is in the forest,
             // and for lanes >= n); the wave minimum of its high word (the diameter) alone decides
             // unless two lanes tie on it. Deaths and forest parents stay in registers (lane t: death
@@ -908,6 +917,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             }
             lds_sync();
             // ---- edge list (i > j, d <= thr), row-major ----
+            relane();
             uint16_t* edges = cx.template sp<uint16_t>(ScratchLayout::edges);
             int n_edges = 0;
             {
@@ -934,6 +944,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             uint8_t* mincof = cx.template sp<uint8_t>(ScratchLayout::mincof);
             uint8_t* mincof_e = cx.template sp<uint8_t>(ScratchLayout::mincof_e);
                     // ---- dim 1: one lane per column (non-tree edge) ----
+                    relane();
             uint32_t* defer = cx.template sp<uint32_t>(ScratchLayout::defer);
             if (dim_max >= 1) {
                 int nna = 0, ndef = 0;
@@ -1018,6 +1029,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                 __syncthreads();
             }
             // ---- dim 2: one lane per column (uncleared triangle) ----
+            relane();
             if (dim_max >= 2 && cx.err == 0) {
                 int nna = 0;
                 // (2a) stream the complex's triangles into a scratch list: each lane owns an edge
@@ -1186,6 +1198,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                 if (bl.counts && lane < 4) at(bl.counts + 4 * gi, lane) = -1;
             } else {
                 // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
+                relane();
                 const double myval = betti_stats35(d0s, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
                 if (feat && lane < 35) at(feat, lane) = myval;
                 if (bl.pairs_out) {

@@ -33,7 +33,11 @@ struct StructMeta {
     float lo32, hi32;
 };
 
-__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+__device__ __forceinline__ int lane_id() {
+    int l = (int)(threadIdx.x & (kWave - 1));
+    asm volatile("" : "+v"(l));
+    return l;
+}
 
 // element i of a per-wave scratch array as (scalar base) + (32-bit byte offset): the load/store
 // takes the base in SGPRs and one vector offset register (global_* vN, s[base]) instead of a
