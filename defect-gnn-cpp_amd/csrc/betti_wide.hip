@@ -62,11 +62,11 @@ __device__ __forceinline__ uint64_t uniw64(uint64_t x) {
     return ((uint64_t)uniw((uint32_t)(x >> 32)) << 32) | uniw((uint32_t)x);
 }
 __device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-// lane-to-lane hand-off through this wave's global scratch in the reduction's hot loop (V list,
-// pivot table, V store): the workgroup barrier, whose fence waits for every outstanding global
-// access of the wave (vmcnt(0)); a wavefront-scope fence instead measured 22.5 -> 21.9
-// structures/s at 10 A (round 3), so the barrier stays
-__device__ __forceinline__ void wave_scratch_sync() { __syncthreads(); }
+// lane-to-lane hand-off through this wave's global scratch (V list, pivot table, V store, lists):
+// a workgroup-scope fence, which waits for every outstanding memory access of the wave
+// (vmcnt(0) lgkmcnt(0)) without a barrier -- the two waves of a workgroup run different phases
+// of different complexes (betti_wide_body)
+__device__ __forceinline__ void wave_scratch_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
 
 // combinatorial index of a packed simplex with nv vertices
 // insert vertex x (not in p) into a packed simplex of nv vertices
@@ -136,6 +136,10 @@ struct WideCx {
     static constexpr bool VREG = KW <= 6 || KW > 8;
     PT vreg = 0;
     bool vspill = false;
+    // the threshold in distance-code space (largest code of a distance <= thr; f32 bits in kF32
+    // mode): the reduction tests common neighbours from the distances alone (no adjacency), with
+    // an all-ones diagonal excluding the simplex's own vertices
+    uint32_t thrc = 0;
 #ifdef DGN_PHASE_TIMING
     uint64_t dg_searches = 0, dg_floor_iters = 0;  // diagnostics: pivot searches and their floor rounds
 #endif
@@ -178,10 +182,11 @@ struct WideCx {
         uint16_t* D16 = sp<uint16_t>(ly.D);
         const uint32_t* Lc = CODED ? bl.rank_codes + slot * bl.rank_stride : nullptr;
         for (int i = lane; i < n * W; i += kWave) adj[i] = 0ull;
-        for (int i = lane; i < n; i += kWave) {  // the diagonal is never read as a distance
-            if (MODE == kC16) D16[(int64_t)i * n + i] = 0;
-            else D[(int64_t)i * n + i] = 0u;
+        for (int i = lane; i < n; i += kWave) {  // all-ones diagonal: no vertex is its own neighbour
+            if (MODE == kC16) D16[(int64_t)i * n + i] = 0xFFFF;
+            else D[(int64_t)i * n + i] = 0xFFFFFFFFu;
         }
+        uint32_t tmax = 0;
         if constexpr (HUGE) wave_scratch_sync();  // the zeroed bitsets (scratch) before the atomics
         else wave_lds_order();
         for (int i = 1; i < n; ++i) {
@@ -199,6 +204,7 @@ struct WideCx {
                         D[(int64_t)j * n + i] = dv;
                     }
                     e = v <= thr;  // sparse_distance_matrix keeps d <= threshold (ripser.cpp:386-395)
+                    if (e) tmax = max(tmax, dv);
                 }
                 const uint64_t b = ballot(e);
                 if (lane == 0) {  // row i, columns j < i
@@ -208,9 +214,10 @@ struct WideCx {
                 if (e) atomicOr((unsigned long long*)&adj[j * W + (i >> 6)], 1ull << (i & 63));
             }
         }
+        thrc = ~wave_min_u32(~tmax);
         // HUGE: the bitsets were built by L2 atomics; the agent-scope fence drops the CU's L1 copies
         if constexpr (HUGE) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-        __syncthreads();
+        wave_scratch_sync();
     }
 
     // ---- dim 0: Prim on F-keys == Kruskal's forest in Ripser's order (ripser.cpp:725-762) ----
@@ -291,7 +298,7 @@ struct WideCx {
                 if ((bits >> lane) & 1ull) edges[off + mask_prefix(bits)] = pack_edge(i, 64 * w + lane);
                 off += __popcll(bits);
             }
-        __syncthreads();
+        wave_scratch_sync();
         return off;
     }
 
@@ -367,10 +374,12 @@ struct WideCx {
     }
 
     // append a non-apparent column (lanes with `na`) to the scratch list
-    __device__ void na_append(bool na, int& nna, uint64_t colkey, uint64_t tau, uint64_t tv, PT colp) {
+    // (the dim-1 list starts at entry 0, the dim-2 list at `base`: both are built before either
+    // dimension is reduced)
+    __device__ void na_append(int base, bool na, int& nna, uint64_t colkey, uint64_t tau, uint64_t tv, PT colp) {
         const uint64_t bal = ballot(na);
         if (na) {
-            const int slot = nna + mask_prefix(bal);
+            const int slot = base + nna + mask_prefix(bal);
             if (slot < ly.na_cap) {
                 sp<uint64_t>(ly.na_key)[slot] = colkey;
                 sp<uint64_t>(ly.na_tau)[slot] = tau;
@@ -420,9 +429,9 @@ struct WideCx {
                 mc_e[bin2(i) + j] = mc;
             }
             // apparent pairs have zero persistence: nothing to emit
-            na_append(na, nna, colkey, best, bestp, colp);
+            na_append(0, na, nna, colkey, best, bestp, colp);
         }
-        __syncthreads();
+        wave_scratch_sync();
         return nna;
     }
 
@@ -434,7 +443,7 @@ struct WideCx {
     // exhausted), so lanes never wait for the longest walk of a round (measured at 10 A: 2.1
     // steps per column on average, 11 for the longest lane of a 64-column round). A fresh
     // triangle's clearing mark and edge lengths are loaded together with its first candidates.
-    __device__ int pass_dim2(int n_edges) {
+    __device__ int pass_dim2(int n_edges, int base) {
         [[maybe_unused]] const int lane = lane_id();
         const uint32_t* edges = sp<uint32_t>(ly.edges);
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
@@ -580,7 +589,7 @@ struct WideCx {
                 }
                 if (done) act = false;
             }
-            na_append(na, nna, colkey, ntau, ntv, ncolp);
+            na_append(base, na, nna, colkey, ntau, ntv, ncolp);
 #ifdef DGN_PHASE_TIMING
             niter += 1;
 #endif
@@ -596,21 +605,37 @@ struct WideCx {
             }
         }
 #endif
-        __syncthreads();
+        wave_scratch_sync();
         return nna;
     }
 
     // ---- non-apparent columns in Ripser's order: bitonic sort, key descending ----
-    __device__ void sort_na(int cnt) {
+    // dim 2 (`cleared`): columns whose triangle is the pivot of a reduced dim-1 column (clearing
+    // marks, set after this list was built) get key 0 and sort last; returns the columns kept
+    __device__ int sort_na(int base, int cnt, bool cleared) {
         const int lane = lane_id();
         int N = 1;
         while (N < cnt) N <<= 1;
-        uint64_t* K = sp<uint64_t>(ly.na_key);
-        uint64_t* T = sp<uint64_t>(ly.na_tau);
-        uint64_t* V = sp<uint64_t>(ly.na_tv);
-        PT* Cc = sp<PT>(ly.na_col);
+        uint64_t* K = sp<uint64_t>(ly.na_key) + base;
+        uint64_t* T = sp<uint64_t>(ly.na_tau) + base;
+        uint64_t* V = sp<uint64_t>(ly.na_tv) + base;
+        PT* Cc = sp<PT>(ly.na_col) + base;
         for (int i = cnt + lane; i < N; i += kWave) K[i] = 0ull;  // padding sorts last
-        __syncthreads();
+        int kept = cnt;
+        if (cleared) {
+            const uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+            for (int i0 = 0; i0 < cnt; i0 += kWave) {
+                const int i = i0 + lane;
+                bool cl = false;
+                if (i < cnt) {
+                    const uint64_t idx = ~K[i] & ((1ull << KS) - 1);
+                    cl = mc_t[idx] == kMcClearedW;
+                    if (cl) K[i] = 0ull;
+                }
+                kept -= __popcll(ballot(cl));
+            }
+        }
+        wave_scratch_sync();
         for (int k = 2; k <= N; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
                 for (int i = lane; i < N; i += kWave) {
@@ -631,8 +656,9 @@ struct WideCx {
                         }
                     }
                 }
-                __syncthreads();
+                wave_scratch_sync();
             }
+        return kept;
     }
 
     // ---- serially resolved pivots: open-addressing hash table (key 0 = empty) ----
@@ -851,13 +877,13 @@ struct WideCx {
 #pragma unroll
                 for (int t = 0; t < KW; ++t) {
                     if (t >= W) break;
-                    uint64_t am = aw(a, t) & aw(b, t);
-                    if (dim == 2) am &= aw(c, t);
                     const int x = 64 * t + k;
                     const uint32_t dd = max(max(ds, dc[t]), max(da[t], db[t]));
                     const uint64_t p = pinsert(dim + 1, s, x);
                     const uint64_t kk = PACKKEY ? pkey(dd, p) : wkey(dd, pidx(dim + 2, p));
-                    if (((am >> k) & 1ull) && kk > floor) {  // x is a common neighbour (so x < n)
+                    // x is a common neighbour iff every distance to s is within the threshold (the
+                    // all-ones diagonal rules out s's own vertices; lanes past n read row n - 1)
+                    if (x < n && dd <= thrc && kk > floor) {
                         if (kk < lmin) {
                             lmin = kk;
                             lcnt = 1;
@@ -905,9 +931,15 @@ struct WideCx {
     }
 
     // ---- the non-apparent columns of one dimension, in Ripser's order ----
-    __device__ void reduce(int dim, int nna) {
+    // the next power of two >= x (the bitonic sort's padded length)
+    __device__ static int pow2ceil(int x) {
+        int N = 1;
+        while (N < x) N <<= 1;
+        return N;
+    }
+    __device__ void reduce(int dim, int nna, int base) {
         const int lane = lane_id();
-        if (nna > ly.na_cap) {
+        if (base + pow2ceil(nna) > ly.na_cap) {
             err |= kENA;
             return;
         }
@@ -931,12 +963,12 @@ struct WideCx {
     do {           \
     } while (0)
 #endif
-        sort_na(nna);
+        nna = sort_na(base, nna, dim == 2);
         WSUB(0);
-        const uint64_t* K = sp<uint64_t>(ly.na_key);
-        const uint64_t* T = sp<uint64_t>(ly.na_tau);
-        const uint64_t* V = sp<uint64_t>(ly.na_tv);
-        const PT* Cc = sp<PT>(ly.na_col);
+        const uint64_t* K = sp<uint64_t>(ly.na_key) + base;
+        const uint64_t* T = sp<uint64_t>(ly.na_tau) + base;
+        const uint64_t* V = sp<uint64_t>(ly.na_tv) + base;
+        const PT* Cc = sp<PT>(ly.na_col) + base;
         PT* vstore = sp<PT>(ly.vstore);
         float2* pairs = sp<float2>(dim == 1 ? ly.p1 : ly.p2);
         int& np = dim == 1 ? n_p1 : n_p2;
@@ -996,7 +1028,14 @@ struct WideCx {
                 if (lane == 0 && np < ly.p_cap) pairs[np] = make_float2(value(birth), value(death));
                 ++np;
             }
-            if (dim == 1 && lane == 0) sp<uint16_t>(ly.mc_t)[pidx(3, tv)] = kMcClearedW;  // clearing
+            if (dim == 1) {  // clearing: tau's column is zero in dim 2 (reset after the dim-2 sort)
+                const uint64_t ti = pidx(3, tv);
+                if (lane == 0) {
+                    sp<uint16_t>(ly.mc_t)[ti] = kMcClearedW;
+                    sp<uint32_t>(ly.cl_list)[ncl] = (uint32_t)ti;
+                }
+                ++ncl;
+            }
             uint64_t m;
             if (v == 0) {
                 m = kLazyW | cp;
@@ -1022,7 +1061,7 @@ struct WideCx {
             ++npiv;
             WSUB(5);
         }
-        __syncthreads();
+        wave_scratch_sync();
 #ifdef DGN_PHASE_TIMING
         if (lane == 0 && bl.phase_cycles) {
             for (int k = 0; k < 6; ++k) atomicAdd(&bl.phase_cycles[16 + k], (unsigned long long)sb[k]);
@@ -1039,7 +1078,7 @@ struct WideCx {
         uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint32_t* used = sp<uint32_t>(ly.h_used);
         for (int i = lane; i < npiv; i += kWave) HK[used[i]] = 0ull;
-        __syncthreads();
+        wave_scratch_sync();
     }
 
     // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) + outputs ----
@@ -1081,70 +1120,88 @@ struct WideCx {
         return true;
     }
 
-    __device__ bool run(int64_t gi, int64_t slot, double weight) {
 #ifdef DGN_PHASE_TIMING
-        // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
-        uint64_t t0 = __builtin_amdgcn_s_memtime();
-        auto stamp = [&](int k) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            if (lane_id() == 0 && bl.phase_cycles) atomicAdd(&bl.phase_cycles[k], (unsigned long long)(t - t0));
-            t0 = t;
-        };
+    // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
+    uint64_t t0 = 0;
+    __device__ void stamp(int k) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (lane_id() == 0 && bl.phase_cycles && k >= 0) atomicAdd(&bl.phase_cycles[k], (unsigned long long)(t - t0));
+        t0 = t;
+    }
 #define WSTAMP(k) stamp(k)
 #else
 #define WSTAMP(k) \
     do {          \
     } while (0)
 #endif
+    // Phase 1, with the workgroup's adjacency buffer held (betti_wide_body): the matrix and the
+    // bitsets, the forest, the edge list and both lane-parallel (apparent) passes; the dim-2 pass
+    // runs before the dim-1 reduction, so the columns the latter clears (their triangles are dim-1
+    // pivots) are dropped from the dim-2 list when it is sorted
+    int nna1 = 0, nna2 = 0, base2 = 0, ncl = 0;
+    __device__ void apparent(int64_t gi, int64_t slot) {
+        WSTAMP(-1);
         load(gi, slot);
         WSTAMP(0);
         prim();
         const int n_edges = edge_list();
         WSTAMP(1);
-        const int nna1 = pass_dim1(n_edges);
+        nna1 = pass_dim1(n_edges);
         WSTAMP(2);
-        reduce(1, nna1);
-        WSTAMP(3);
-        __syncthreads();  // clearing marks complete before the dim-2 pass reads them
-        if (err == 0u) {
-            const int nna2 = pass_dim2(n_edges);
-            WSTAMP(4);
-            reduce(2, nna2);
-            WSTAMP(5);
+        base2 = pow2ceil(nna1);
+        nna2 = pass_dim2(n_edges, base2);
+        WSTAMP(4);
 #ifdef DGN_PHASE_TIMING
-            if (lane_id() == 0 && bl.phase_cycles) {
-                atomicAdd(&bl.phase_cycles[8], (unsigned long long)nna1);
-                atomicAdd(&bl.phase_cycles[9], (unsigned long long)nna2);
-                atomicAdd(&bl.phase_cycles[10], (unsigned long long)n_edges);
-            }
-#endif
-        } else {
-            // no dim-2 pass consumes the clearing marks: erase every triangle entry
-            uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
-            const int64_t nt = (int64_t)bin3((uint64_t)n);
-            for (int64_t t = lane_id(); t < nt; t += kWave) mc_t[t] = kMcNoneW;
+        if (lane_id() == 0 && bl.phase_cycles) {
+            atomicAdd(&bl.phase_cycles[8], (unsigned long long)nna1);
+            atomicAdd(&bl.phase_cycles[9], (unsigned long long)nna2);
+            atomicAdd(&bl.phase_cycles[10], (unsigned long long)n_edges);
         }
-        __syncthreads();
+#endif
+    }
+    // Phase 2, from scratch alone (no LDS): the two reductions, the statistics and the outputs.
+    // True when the complex's outputs were written.
+    __device__ bool reduce_finish(int64_t gi, double weight) {
+        reduce(1, nna1, 0);
+        WSTAMP(3);
+        if (err == 0u) reduce(2, nna2, base2);
+        WSTAMP(5);
+        // the dim-1 clearing marks were read by the dim-2 sort; reset them for the next complex
+        // (every other min-cofacet entry a later complex reads is rewritten by its dim-2 pass)
+        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+        const uint32_t* cl = sp<uint32_t>(ly.cl_list);
+        for (int i = lane_id(); i < ncl; i += kWave) mc_t[cl[i]] = kMcNoneW;
+        wave_scratch_sync();
         const bool ok = finish(gi, weight);
-        __syncthreads();
+        wave_scratch_sync();
         WSTAMP(6);
-#undef WSTAMP
         return ok;
     }
+#undef WSTAMP
 };
 
 template <int KW, int MODE>
 __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const WideLayout& ly) {
-    // dynamic LDS (wide_lds_bytes): adjacency [nmax][ceil(nmax / 64)] u64, forest parents
-    // [nmax] u16
-    // [nmax] u16 (HUGE: the parents only, the adjacency lives in the wave's scratch at ly.adj)
+    // dynamic LDS (wide_lds_bytes), one buffer per workgroup of kWideWaves waves: the buffer token
+    // (u64), the adjacency [nmax][ceil(nmax / 64)] u64 and the forest parents [nmax] u16 (HUGE:
+    // the parents only; the adjacency lives in each wave's scratch at ly.adj). A wave holds the
+    // buffer from its complex's load through the two apparent passes, then reduces from scratch
+    // alone while the other wave loads its next complex: twice the waves per CU for the LDS of one
+    // complex (the reductions, about half of a 10 A complex's time, read no LDS).
     extern __shared__ uint64_t wide_lds[];
     constexpr bool kHugeMode = MODE == kHuge;
     const int64_t ww = (ly.nmax + 63) / 64;
     const int lane = lane_id();
-    uint8_t* scr = ly.base + (int64_t)blockIdx.x * ly.total;
-    uint64_t* adj = kHugeMode ? reinterpret_cast<uint64_t*>(scr + ly.adj) : wide_lds;
-    uint16_t* par = reinterpret_cast<uint16_t*>(kHugeMode ? wide_lds : wide_lds + ly.nmax * ww);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int64_t slot = (int64_t)blockIdx.x * kWideWaves + w;
+    uint32_t* tok = reinterpret_cast<uint32_t*>(wide_lds);
+    if (threadIdx.x == 0) *tok = 0u;  // the buffer starts free (the one workgroup barrier)
+    __syncthreads();
+    if (slot >= ly.slots) return;  // the last workgroup of an odd wave count
+    uint64_t* lds = wide_lds + 1;
+    uint8_t* scr = ly.base + slot * ly.total;
+    uint64_t* adj = kHugeMode ? reinterpret_cast<uint64_t*>(scr + ly.adj) : lds;
+    uint16_t* par = reinterpret_cast<uint16_t*>(kHugeMode ? lds : lds + ly.nmax * ww);
     const int64_t total = (int64_t)*bl.wide_len;
     for (;;) {
         // wave-uniform dequeue without a branch on the lane (see betti_kernels.hip): every lane adds
@@ -1163,24 +1220,34 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
         } else {
             WideCx<KW, MODE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
             if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+            // take the buffer: every lane tries the same compare-and-swap, the wave holds it when one
+            // of its lanes won (a uniform ballot; no branch on the lane, see the dequeue)
+            for (;;) {
+                const uint32_t prev = atomicCAS(tok, 0u, 1u);
+                if (ballot(prev == 0u)) break;
+                __builtin_amdgcn_s_sleep(4);
+            }
+            cx.apparent(gi, wi);
+            wave_scratch_sync();  // every LDS access of the apparent phase done
+            *tok = 0u;            // release (every lane stores the same word)
             // dgn_debug_retry_count counts the complexes a retry launch reduced successfully
-            const bool ok = cx.run(gi, wi, bl.weight ? bl.weight[gi] : 1.0);
+            const bool ok = cx.reduce_finish(gi, bl.weight ? bl.weight[gi] : 1.0);
             if (ok && bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
         }
     }
 }
 
 template <int KW, int MODE>
-__global__ __launch_bounds__(kWave) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
+__global__ __launch_bounds__(kWave * kWideWaves) void betti_wide_kernel(BettiLaunch bl, WideLayout ly) {
     betti_wide_body<KW, MODE>(bl, ly);
 }
 #ifndef DGN_WIDE_C16_WAVES
-#define DGN_WIDE_C16_WAVES 3  // waves per SIMD the u16-code instantiations are compiled for
+#define DGN_WIDE_C16_WAVES 5  // waves per SIMD the u16-code instantiations are compiled for
 #endif
 // the u16-code instantiations (the 10 A path) with a register budget for DGN_WIDE_C16_WAVES waves
 // per SIMD: resident waves are what this latency-bound kernel scales with
 template <int KW>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(DGN_WIDE_C16_WAVES, DGN_WIDE_C16_WAVES)))
+__global__ __launch_bounds__(kWave * kWideWaves) __attribute__((amdgpu_waves_per_eu(DGN_WIDE_C16_WAVES)))
 void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
     betti_wide_body<KW, kC16>(bl, ly);
 }
@@ -1204,10 +1271,10 @@ WideKernel wide_kernel_for(int nmax, bool c16) {
     return betti_wide_kernel<32, kHuge>;              // 1025..2048 points: HUGE
 }
 
-size_t wide_lds_bytes(int nmax) {
+size_t wide_lds_bytes(int nmax) {  // per workgroup: token, adjacency, parents
     const int64_t ww = (nmax + 63) / 64;
-    if (nmax > kWideBigPoints) return (size_t)(8 * ((nmax + 3) / 4));  // parents only
-    return (size_t)(8 * (nmax * ww + (nmax + 3) / 4));
+    if (nmax > kWideBigPoints) return (size_t)(8 * (1 + (nmax + 3) / 4));  // parents only
+    return (size_t)(8 * (1 + nmax * ww + (nmax + 3) / 4));
 }
 
 }  // namespace
@@ -1253,10 +1320,9 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
     l.na_tau = take(8 * cap);
     l.na_tv = take(8 * cap);
     l.na_col = take(pt * cap);
-    l.na_perm = take(4 * cap);
+    l.cl_list = take(4 * cap);  // triangle indices of the dim-1 clearing marks
     l.vstore = take(pt * (int64_t)l.vs_cap);
     l.vlist = take(pt * (int64_t)l.vl_cap);
-    l.vdiam = take(4 * (int64_t)l.vl_cap);
     l.h_key = take(8 * 2 * cap);
     l.h_meta = take(8 * 2 * cap);
     l.h_used = take(4 * cap);
@@ -1279,17 +1345,20 @@ int betti_wide_resident_waves(int device, int nmax, bool c16) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, c16), kWave, wide_lds_bytes(nmax)) !=
-            hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, c16), kWave * kWideWaves,
+                                                     wide_lds_bytes(nmax)) != hipSuccess ||
         per_cu <= 0)
-        per_cu = 2;
-    return prop.multiProcessorCount * per_cu;
+        per_cu = 1;
+    return prop.multiProcessorCount * per_cu * kWideWaves;
 }
 
 hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
     if (waves <= 0) return hipSuccess;
-    hipLaunchKernelGGL(wide_kernel_for(l.nmax, b.rank_codes != nullptr && l.nmax <= kC16MaxPoints), dim3((unsigned)waves),
-                       dim3(kWave), wide_lds_bytes(l.nmax), st, b, l);
+    WideLayout lw = l;
+    lw.slots = waves;  // scratch slots allocated: a wave past them leaves at once
+    hipLaunchKernelGGL(wide_kernel_for(l.nmax, b.rank_codes != nullptr && l.nmax <= kC16MaxPoints),
+                       dim3((unsigned)((waves + kWideWaves - 1) / kWideWaves)), dim3(kWave * kWideWaves),
+                       wide_lds_bytes(l.nmax), st, b, lw);
     return hipGetLastError();
 }
 

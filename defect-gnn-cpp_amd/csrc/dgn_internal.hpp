@@ -154,12 +154,14 @@ constexpr int kWideBigPoints = 1024;
 constexpr int kWideRegular = 512;
 constexpr int kC16MaxPoints = 362;  // C(362, 2) < 2^16: u16 rank codes (wide launch)
 constexpr int kWideMaxGrow = 3;     // capacity-retry layout levels: tables of 2^24 .. 2^30 entries
+constexpr int kWideWaves = 2;       // waves per wide workgroup, sharing one LDS adjacency buffer
 struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
     int64_t total;
     int32_t nmax, na_cap, p_cap, h_cap, vs_cap, vl_cap;
+    int32_t slots;  // scratch slots of the launch (set by launch_betti_wide)
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
-    int64_t D, mc_e, mc_t, edges, adj, na_key, na_tau, na_tv, na_col, na_perm, vstore, vlist, vdiam, h_key, h_meta,
+    int64_t D, mc_e, mc_t, edges, adj, na_key, na_tau, na_tv, na_col, cl_list, vstore, vlist, h_key, h_meta,
         h_used, p1, p2, d0;
 };
 // cap_limit > 0 (tests, DGN_DEBUG_WIDE_CAP): the regular layout's column / pivot / pair tables

@@ -7,6 +7,8 @@ Writes (profiles/):
   r04_mfma.json                                distance kernel MFMA counters + derived rates
   r04_rc10_wide.json                           the 10 A wide kernel: time, HBM bytes and SQ mix per complex
   r04_side_graph.json                          per-kernel medians of BASELINE configs 2 and 5 (f32 / f64 RBF)
+  r04_narrow_phases_stop.json                  betti_kernel<44> instruction counts cut after each phase
+                                               (stop-at builds, -DDGN_STOP_AT=k; gpurun_out/r04_stop)
 SQ cycle counters (SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_WAIT_*, SQ_ACTIVE_INST_*) are in quad-cycles
 (MI355X_MICROARCH.md "s_memtime tick vs SQ PMC units"); instruction counters are per wave instruction.
 """
@@ -168,5 +170,28 @@ def main():
         json.dump(out, open(os.path.join(HERE, "r04_side_graph.json"), "w"), indent=1)
 
 
+def stop_phases():
+    """Cumulative instruction counts of betti_kernel<44> when the kernel stops after phase k
+    (DGN_STOP_AT builds of the early round-4 source, tools/betti_run.py fcc 4 512 5.0 1): the
+    difference between consecutive rows is what each phase issues."""
+    import re
+    sd = os.path.join(os.path.dirname(D), "r04_stop")
+    if not os.path.isdir(sd):
+        return
+    names = {"stop1": "load (triangle -> LDS matrix)", "stop2": "+ adjacency, Prim, edge list",
+             "stop3": "+ dim-1 apparent pass", "stop4": "+ dim-1 reduction", "stop5": "+ dim-2 triangle enumeration",
+             "stop6": "+ dim-2 apparent pass", "base": "full kernel (+ dim-2 reduction, statistics)"}
+    out = {"workload": "512 FCC-256 structures at 5 A (131,072 complexes); cumulative counts per stop point",
+           "rows": {}}
+    for k, label in names.items():
+        txt = open(os.path.join(sd, f"{k}.txt")).read()
+        m = re.search(r"void dgn::betti_kernel<44>\n((?:\s+\S+\s+\S+\s+\(n=\d+\)\n)+)", txt)
+        c = {ln.split()[0]: float(ln.split()[1]) for ln in m.group(1).strip().split("\n")}
+        out["rows"][k] = {"phase": label, **{x: c.get(x) for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_BRANCH",
+                                                                  "SQ_INSTS_LDS", "SQ_INSTS_VMEM")}}
+    json.dump(out, open(os.path.join(HERE, "r04_narrow_phases_stop.json"), "w"), indent=1)
+
+
 if __name__ == "__main__":
+    stop_phases()
     main()
