@@ -437,19 +437,36 @@ struct WideCx {
 
     // ---- dim 2: one lane per column (uncleared triangle), a per-lane work queue ----
     static constexpr int kStep = DGN_WIDE_STEP;  // candidates per walk step (distance reads in flight)
-    // Each lane owns an edge (a > b) of the edge list and the triangles (a, b, c), c < b, of its
-    // common neighbours; it walks one triangle's candidate cofacets four per step and takes its
-    // next triangle as soon as the walk ends (zero-persistence cofacet found, or candidates
-    // exhausted), so lanes never wait for the longest walk of a round (measured at 10 A: 2.1
-    // steps per column on average, 11 for the longest lane of a 64-column round). A fresh
-    // triangle's clearing mark and edge lengths are loaded together with its first candidates.
+    // position of the r-th (0-based) set bit of x (r < popcount(x))
+    __device__ static int select_bit(uint64_t x, int r) {
+        int pos = 0;
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) {
+            const int cnt = __popcll(x & ((1ull << sh) - 1ull));
+            const bool up = r >= cnt;
+            r = up ? r - cnt : r;
+            x = up ? x >> sh : x;
+            pos += up ? sh : 0;
+        }
+        return pos;
+    }
+    // The triangles (a, b, c), c < b a common neighbour of the edge a > b, are dealt in edge-list
+    // order from a wave-uniform cursor: a lane whose walk ended (zero-persistence cofacet found,
+    // or candidates exhausted) takes the next triangle at once, so lanes never wait for the
+    // longest walk of a round (10 A: 2.1 steps per column on average, 11 for the longest lane of
+    // a 64-column round), and at any time the wave's lanes hold consecutive triangles -- mostly of
+    // one or two edges, so their reads of rows a and b fall in a few lines (round 3 gave each
+    // lane its own edge: 64 different rows a, b per load). A fresh triangle's clearing mark and
+    // edge lengths are loaded together with its first candidates.
     __device__ int pass_dim2(int n_edges, int base) {
         [[maybe_unused]] const int lane = lane_id();
         const uint32_t* edges = sp<uint32_t>(ly.edges);
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
-        int nna = 0, next_edge = 0;
-        int ea = 0, eb = 0, tw = -1;  // the lane's edge (a > b) and the word of its next c < b
-        uint64_t tm = 0;              // remaining c of that word
+        int nna = 0;
+        // the cursor (uniform): edge ce = (ca > cb), word cw of its c < cb, the c's not yet dealt
+        int ce = -1, ca = 0, cb = 0, cw = 0;
+        uint64_t cm = 0;
+        int ea = 0, eb = 0;  // the lane's triangle's edge
         bool act = false, fresh = false;
         int c = 0, w = 0, bk = 0;
         uint64_t m = 0, tidx = 0;
@@ -461,36 +478,38 @@ struct WideCx {
         uint64_t nsteps = 0, niter = 0, ncols = 0;
 #endif
         for (;;) {
-            // (1) lanes without a triangle take the next c of their edge, or a new edge
+            // (1) lanes without a triangle take the next ones from the cursor, in order
             for (;;) {
-                while (!act && tm == 0ull && tw >= 0) {  // next word of the current edge
-                    ++tw;
-                    if (64 * tw >= eb) {
-                        tw = -1;
-                        break;
+                uint64_t need = ballot(!act);
+                if (!need) break;
+                while (cm == 0ull && ce < n_edges) {  // advance the cursor to the next word with a c
+                    if (ce >= 0 && 64 * (cw + 1) < cb) {
+                        ++cw;
+                    } else {
+                        if (++ce >= n_edges) break;
+                        const uint32_t ed = uniw(edges[ce]);
+                        ca = (int)(ed >> VB);
+                        cb = (int)(ed & VM);
+                        cw = 0;
                     }
-                    tm = aw(ea, tw) & aw(eb, tw);
-                    const int lim = eb - 64 * tw;
-                    if (lim < 64) tm &= (1ull << lim) - 1ull;
+                    uint64_t mm = uniw64(aw(ca, cw) & aw(cb, cw));
+                    const int lim = cb - 64 * cw;
+                    if (lim < 64) mm &= (1ull << lim) - 1ull;
+                    cm = mm;
                 }
-                const bool need = !act && tm == 0ull;
-                const uint64_t bal = ballot(need);
-                if (!bal || next_edge >= n_edges) break;
-                const int e = next_edge + mask_prefix(bal);
-                if (need && e < n_edges) {
-                    const uint32_t ed = edges[e];
-                    ea = (int)(ed >> VB);
-                    eb = (int)(ed & VM);
-                    tw = 0;
-                    tm = aw(ea, 0) & aw(eb, 0);
-                    if (eb < 64) tm &= (1ull << eb) - 1ull;
+                if (cm == 0ull) break;  // every triangle dealt
+                const int p = __popcll(cm), q = __popcll(need);
+                const int r = mask_prefix(need);  // this lane's rank among the lanes to fill
+                if (!act && r < p) {
+                    c = 64 * cw + select_bit(cm, r);
+                    ea = ca;
+                    eb = cb;
+                    act = fresh = true;
                 }
-                next_edge += __popcll(bal);
+                // drop the dealt c's (the lowest min(p, q) bits)
+                cm = q >= p ? 0ull : cm & ~((1ull << select_bit(cm, q)) - 1ull);
             }
-            if (!act && tm != 0ull) {
-                c = 64 * tw + __ffsll((unsigned long long)tm) - 1;
-                tm &= tm - 1ull;
-                act = fresh = true;
+            if (fresh) {
                 tidx = bin3(ea) + bin2(eb) + c;
                 colp = ((PT)ea << (2 * VB)) | ((PT)eb << VB) | (PT)c;
                 w = W - 1;
