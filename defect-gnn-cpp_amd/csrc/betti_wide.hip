@@ -463,9 +463,15 @@ struct WideCx {
         const uint32_t* edges = sp<uint32_t>(ly.edges);
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
         int nna = 0;
-        // the cursor (uniform): edge ce = (ca > cb), word cw of its c < cb, the c's not yet dealt
+        // the cursor (uniform): edge ce = (ca > cb), word cw of its c < cb, the c's not yet dealt;
+        // the edge list is read 64 entries at a time (lane i: entry eb0 + i) and the next batch
+        // is prefetched when the cursor enters the current one, so advancing to an edge is a
+        // readlane, not a dependent scratch load
         int ce = -1, ca = 0, cb = 0, cw = 0;
         uint64_t cm = 0;
+        int eb0 = 0;
+        uint32_t ebuf = lane < n_edges ? edges[lane] : 0u;
+        uint32_t enext = kWave + lane < n_edges ? edges[kWave + lane] : 0u;
         int ea = 0, eb = 0;  // the lane's triangle's edge
         bool act = false, fresh = false;
         int c = 0, w = 0, bk = 0;
@@ -487,7 +493,12 @@ struct WideCx {
                         ++cw;
                     } else {
                         if (++ce >= n_edges) break;
-                        const uint32_t ed = uniw(edges[ce]);
+                        if (ce >= eb0 + kWave) {  // next batch (already in flight), prefetch the one after
+                            eb0 += kWave;
+                            ebuf = enext;
+                            enext = eb0 + kWave + lane < n_edges ? edges[eb0 + kWave + lane] : 0u;
+                        }
+                        const uint32_t ed = rlw(ebuf, ce - eb0);
                         ca = (int)(ed >> VB);
                         cb = (int)(ed & VM);
                         cw = 0;
