@@ -483,12 +483,14 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
         wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap);
         // as many waves as the device keeps resident (dynamic LDS sized by
-        // max_points), each with its own scratch, within half of the free HBM (288 GB per MI355X;
-        // at least 8 GB)
+        // max_points), each with its own scratch, within half of the HBM that is free or already
+        // this workspace's (288 GB per MI355X; at least 8 GB) -- counting the workspace in the pool
+        // keeps the wave count, hence the layout, the same from one call to the next (a changed
+        // layout re-initialises every wave's tables)
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t budget =
-            std::max<int64_t>(int64_t(8) << 30, (int64_t)(free_b / 2) + (int64_t)c->b_wide.bytes);
+            std::max<int64_t>(int64_t(8) << 30, ((int64_t)free_b + (int64_t)c->b_wide.bytes) / 2);
         const int64_t resident =
             betti_wide_resident_waves(c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
