@@ -29,8 +29,10 @@ struct StructMeta {
     double band;     // |d2_approx - d2| bound of the fixed-point nearest-image distance (x64 margin)
     // the one-image count pass's packed-f32 prefilter (count_one_image): lattice * 2^-32 in f32 and
     // the d2 window (rc^2 -+ its rigorous band) outside which the f32 value decides
+    // (unscaled for `few` structures, whose f32 displacements are fractions, not fixed point)
     float lf[9];
     float lo32, hi32;
+    int32_t few;     // not one, every H_k < 1 and nref == 2: at most two images per axis (search_staged_few)
 };
 
 __device__ __forceinline__ int lane_id() {

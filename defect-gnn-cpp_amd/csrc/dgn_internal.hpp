@@ -16,6 +16,8 @@ constexpr int kCellMax = 4096;            // cells per structure (cell list, nat
 constexpr int kScanThreads = 1024;
 constexpr int kRing = 128;                // per-wave candidate ring (one-image prefilter)
 constexpr int kMaskWords = kStage / 64;   // hit-mask words per query atom (staged structures)
+constexpr int kFewMaskWords = 8;          // `few` structures of <= 64 atoms: a hit word per image combination
+static_assert(kFewMaskWords <= kMaskWords, "few masks use the per-atom mask slots");
 
 // graph error bits (Scalars::error_flag), decoded in dgn_api.cpp
 constexpr uint32_t kGErrCap = 1u << 0;       // more candidates than the emit capacity

@@ -66,10 +66,11 @@ __global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict
     m.R[0] = c00 * id; m.R[1] = c01 * id; m.R[2] = c02 * id;
     m.R[3] = c10 * id; m.R[4] = c11 * id; m.R[5] = c12 * id;
     m.R[6] = c20 * id; m.R[7] = c21 * id; m.R[8] = c22 * id;
-    bool one = true;
+    bool one = true, few = true;
     for (int k = 0; k < 3; ++k) {
         m.H[k] = rc * sqrt(m.R[k] * m.R[k] + m.R[3 + k] * m.R[3 + k] + m.R[6 + k] * m.R[6 + k]) + 1e-9;
         one = one && m.H[k] < 0.5;
+        few = few && m.H[k] < 1.0;
     }
     // Eigen Matrix3d row norm: x0 + (x1 + x2) (fixed-size unrolled redux), neighbor_list.cpp:69
     double lmin = 1e300;
@@ -84,6 +85,9 @@ __global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict
     // norm); the 5^3 image-offset table of the staged search relies on it
     m.one = (one && m.nref == 2) ? 1 : 0;
     m.cells = (m.one && m.natoms > kStage) ? 1 : 0;
+    // every H_k < 1 (rc below every perpendicular width, so nref == 2 as well): at most two images
+    // per axis can reach rc; staged structures take search_staged_few
+    m.few = (!m.one && few && m.nref == 2) ? 1 : 0;
     m.diag = (L[1] == 0.0 && L[2] == 0.0 && L[3] == 0.0 && L[5] == 0.0 && L[6] == 0.0 && L[7] == 0.0) ? 1 : 0;
     // the fixed-point coordinates truncate at 2^-32: the nearest-image displacement is off by at
     // most 2^-31 (|a| + |b| + |c|) per component, d2 by 2 rc times that (for d <= rc); 64x margin
@@ -98,16 +102,18 @@ __global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict
     //   axis (conversion of the 32-bit fraction, the rounded f32 lattice, product, two sums),
     //   2 sqrt(3) R eps + 3 eps^2 on the square (R = rc + 1e-3 bounds |d|), 3 * 2^-24 R^2 for the
     //   f32 square and sums, 2^-20 rc^2 for rounding the thresholds; the sum is doubled.
+    //   `few` structures (search_staged_few) convert the fixed-point fraction (|D| <= 0.5) and add
+    //   the +-1 shift in f32 (|f| < 1, one more rounding): eps <= 8 * 2^-24 * sum|L| covers it.
     {
         const double rc2 = rc * rc;
         double lsum = 0.0;
         for (int k = 0; k < 9; ++k) lsum += fabs(L[k]);
-        const double eps = 5.0 * 0x1p-24 * 0.5 * lsum, R = sqrt(rc2) + 1e-3;
+        const double eps = (m.few ? 8.0 * 0x1p-24 : 5.0 * 0x1p-24 * 0.5) * lsum, R = sqrt(rc2) + 1e-3;
         const double band32 = 2.0 * (m.band + 2.0 * 1.7320508075688772 * R * eps + 3.0 * eps * eps +
                                      3.0 * 0x1p-24 * R * R + 0x1p-20 * rc2);
         m.lo32 = (float)(rc2 - band32);
         m.hi32 = (float)(rc2 + band32);
-        for (int k = 0; k < 9; ++k) m.lf[k] = (float)(L[k] * 0x1p-32);
+        for (int k = 0; k < 9; ++k) m.lf[k] = (float)(L[k] * (m.few ? 1.0 : 0x1p-32));
     }
     for (int k = 0; k < 3; ++k) m.nc[k] = 1;
     if (m.cells) {
@@ -155,7 +161,7 @@ __global__ __launch_bounds__(1024) void prep_atoms_kernel(const StructMeta* __re
     const StructMeta& sm = meta[b];
     const int64_t first = sm.first;
     const int natoms = sm.natoms;
-    const bool one = sm.one != 0;
+    const bool one = sm.one != 0 || sm.few != 0;  // fixed-point coordinates (10-bit floors) in use
     for (int t = tid; t < natoms; t += blockDim.x) {
         atom_struct[first + t] = (int32_t)b;
         if (one) {
@@ -337,7 +343,7 @@ __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const Stag
                     st.y[t] = p[1];
                     st.z[t] = p[2];
                 }
-                if (M.one) {
+                if (M.one || M.few) {
                     int sf[3];
                     uint32_t W[3];
                     for (int k = 0; k < 3; ++k) frac_fixed(M.R, k, p, sf[k], W[k]);
@@ -345,7 +351,7 @@ __device__ __forceinline__ void for_block_atoms(const GraphLaunch& g, const Stag
                     st.fx[t] = v;
                 }
             }
-            if (M.one && st.offt && threadIdx.x < 125) {
+            if ((M.one || M.few) && st.offt && threadIdx.x < 125) {
                 const int t = threadIdx.x;
                 const double na = (double)(t / 25 - 2), nb = (double)((t / 5) % 5 - 2), nc = (double)(t % 5 - 2);
                 double o[3];
@@ -397,20 +403,11 @@ __device__ __forceinline__ void unpack_jimg(uint64_t key, int& j, int& na, int& 
 // the wrap of W_j - W_q) and the reference arithmetic (offset from the staged 5^3 table, |n| <=
 // nref = 2) give the exact d2.
 // posj(j, p) yields atom j's position (LDS stage or global memory: the same doubles)
+// The exact d2 of atom j's image n (|n_k| <= 2 when inr; otherwise image 0 is evaluated and the
+// caller discards the value): offset from the staged 5^3 table or the table's arithmetic.
 template <class PosJ>
-__device__ __forceinline__ double exact_one_at(const StructMeta& M, const DGN_LDS f64x4* offt, const u32x4 fq,
-                                               const u32x4 fj, PosJ&& posj, int j, const double q[3], int n[3],
-                                               bool& inr) {
-    inr = true;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const uint32_t wj = k == 0 ? fj.x : (k == 1 ? fj.y : fj.z);
-        const uint32_t wq = k == 0 ? fq.x : (k == 1 ? fq.y : fq.z);
-        const int dw = (int)(wj - wq);
-        const int carry = (int)(wj >= wq) - (int)(dw >= 0);
-        n[k] = (floor_of(fq.w, k) - floor_of(fj.w, k)) - carry;
-        inr = inr && (uint32_t)(n[k] + 2) <= 4u;  // |n| <= nref = 2
-    }
+__device__ __forceinline__ double exact_at_n(const StructMeta& M, const DGN_LDS f64x4* offt, PosJ&& posj, int j,
+                                             const double q[3], const int n[3], bool inr) {
     f64x4 o;
     if (offt) {
         o = offt[inr ? (n[0] + 2) * 25 + (n[1] + 2) * 5 + (n[2] + 2) : 62];
@@ -425,6 +422,22 @@ __device__ __forceinline__ double exact_one_at(const StructMeta& M, const DGN_LD
     const double p0 = pj[0] + o.x, p1 = pj[1] + o.y, p2 = pj[2] + o.z;  // p = pos + offset
     const double e0 = q[0] - p0, e1 = q[1] - p1, e2 = q[2] - p2;
     return ((0.0 + e0 * e0) + e1 * e1) + e2 * e2;  // L2_Simple_Adaptor accumulation
+}
+template <class PosJ>
+__device__ __forceinline__ double exact_one_at(const StructMeta& M, const DGN_LDS f64x4* offt, const u32x4 fq,
+                                               const u32x4 fj, PosJ&& posj, int j, const double q[3], int n[3],
+                                               bool& inr) {
+    inr = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t wj = k == 0 ? fj.x : (k == 1 ? fj.y : fj.z);
+        const uint32_t wq = k == 0 ? fq.x : (k == 1 ? fq.y : fq.z);
+        const int dw = (int)(wj - wq);
+        const int carry = (int)(wj >= wq) - (int)(dw >= 0);
+        n[k] = (floor_of(fq.w, k) - floor_of(fj.w, k)) - carry;
+        inr = inr && (uint32_t)(n[k] + 2) <= 4u;  // |n| <= nref = 2
+    }
+    return exact_at_n(M, offt, posj, j, q, n, inr);
 }
 __device__ __forceinline__ double exact_one(const StructMeta& M, const StageView& st, const u32x4 fq, const u32x4 fj,
                                             int j, const double q[3], int n[3], bool& inr) {
@@ -606,11 +619,193 @@ __device__ __forceinline__ int collect_mask_hits(const DGN_LDS uint64_t* mask, i
         const uint64_t wv = mask[t];  // broadcast read
         const uint64_t word = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(wv >> 32)) << 32) |
                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wv);
-        if ((word >> lane) & 1ull) hit[m + mask_prefix(word)] = (uint32_t)(64 * t + lane);
+        const int slot = m + mask_prefix(word);
+        if (((word >> lane) & 1ull) && slot < kWave) hit[slot] = (uint32_t)(64 * t + lane);  // callers use <= 64
         m += __popcll(word);
     }
     wave_lds_sync();
     return m;
+}
+// the same for a `few` structure of <= 64 atoms: word c = combination c's hits (count_few), entries
+// (c << 16 | j) in combination order
+__device__ __forceinline__ int collect_few_hits(const DGN_LDS uint64_t* mask, DGN_LDS uint32_t* hit) {
+    const int lane = lane_id();
+    int m = 0;
+#pragma unroll
+    for (int c = 0; c < kFewMaskWords; ++c) {
+        const uint64_t wv = mask[c];
+        const uint64_t word = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(wv >> 32)) << 32) |
+                              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wv);
+        const int slot = m + mask_prefix(word);
+        if (((word >> lane) & 1ull) && slot < kWave) hit[slot] = ((uint32_t)c << 16) | (uint32_t)lane;
+        m += __popcll(word);
+    }
+    wave_lds_sync();
+    return m;
+}
+
+// (1b) staged structure with every H_k < 1 (`few`: cells wider than rc but narrower than 2 rc,
+// e.g. config 2's SC-64 at 5 A, H = 0.54). Per axis at most two images of atom j can reach rc:
+// the nearest one (D_k of (1), image n0_k) and, when 1 - |D_k| <= H_k, the next one on the other
+// side (D_k + s_k, s_k = -sign(D_k), image n0_k + s_k) — at most 2^3 (atom, image) candidates,
+// each decided in f32 from the fixed-point fractions (window [lo32, hi32], prep_meta_kernel) with
+// the borderline ones sent to the exact reference test. The general search (3) enumerates the same
+// images through f64 slab bounds and per-lane image loops.
+struct FewLane {
+    float f[3][2];  // fractional displacement of option 0 / 1 per axis
+    int n0[3];      // option 0's image per axis
+    uint32_t up;    // bit k: axis k's option-1 shift is +1 (else -1)
+    uint32_t ok;    // bit 2k + o: option o of axis k within H_k (+ f32 slack) and |n| <= nref = 2
+};
+__device__ __forceinline__ FewLane few_lane(const float h[3], const u32x4 fq, const u32x4 fj) {
+    FewLane r;
+    r.up = 0;
+    r.ok = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t wj = k == 0 ? fj.x : (k == 1 ? fj.y : fj.z);
+        const uint32_t wq = k == 0 ? fq.x : (k == 1 ? fq.y : fq.z);
+        const int dw = (int)(wj - wq);
+        const int carry = (int)(wj >= wq) - (int)(dw >= 0);
+        const int n0 = (floor_of(fq.w, k) - floor_of(fj.w, k)) - carry;
+        const int s = dw >= 0 ? -1 : 1;
+        const float f0 = (float)dw * 0x1p-32f;
+        const float f1 = f0 + (float)s;
+        r.f[k][0] = f0;
+        r.f[k][1] = f1;
+        r.n0[k] = n0;
+        r.up |= s > 0 ? 1u << k : 0u;
+        r.ok |= (__builtin_fabsf(f0) <= h[k] && (uint32_t)(n0 + 2) <= 4u) ? 1u << (2 * k) : 0u;
+        r.ok |= (__builtin_fabsf(f1) <= h[k] && (uint32_t)(n0 + s + 2) <= 4u) ? 2u << (2 * k) : 0u;
+    }
+    return r;
+}
+// combination c (bit k = axis k's option) admissible for this lane
+__device__ __forceinline__ bool few_combo_ok(uint32_t ok, int c) {
+    return ((ok >> (c & 1)) & (ok >> (2 + ((c >> 1) & 1))) & (ok >> (4 + ((c >> 2) & 1))) & 1u) != 0;
+}
+__device__ __forceinline__ void few_image(const FewLane& r, int c, int n[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) n[k] = r.n0[k] + (((c >> k) & 1) ? (((r.up >> k) & 1) ? 1 : -1) : 0);
+}
+// approximate |displacement|^2 of combination c (f32 lattice rows M.lf, unscaled for `few`)
+__device__ __forceinline__ float few_d2(const StructMeta& M, const FewLane& r, int c) {
+    const float u0 = r.f[0][c & 1], u1 = r.f[1][(c >> 1) & 1], u2 = r.f[2][(c >> 2) & 1];
+    const float* L = M.lf;
+    float dx, dy, dz;
+    if (M.diag) {
+        dx = u0 * L[0];
+        dy = u1 * L[4];
+        dz = u2 * L[8];
+    } else {
+        dx = __builtin_fmaf(u2, L[6], __builtin_fmaf(u1, L[3], u0 * L[0]));
+        dy = __builtin_fmaf(u2, L[7], __builtin_fmaf(u1, L[4], u0 * L[1]));
+        dz = __builtin_fmaf(u2, L[8], __builtin_fmaf(u1, L[5], u0 * L[2]));
+    }
+    return __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+}
+// conservative f32 half-widths: H_k plus the f32 error of the displacement (<= 2^-23)
+__device__ __forceinline__ void few_halfwidths(const StructMeta& M, float h[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) h[k] = (float)M.H[k] + 0x1p-20f;
+}
+
+// Count pass on a staged `few` structure: sure hits (below lo32) are counted from the f32 value,
+// borderline ones take the exact test. The self image (j == li, n = 0, d2 = 0) is skipped exactly
+// when the reference skips it (sqrt(0) < eps).
+// mask_words (structures of <= 64 atoms, or null): word c = the hit ballot of combination c, which
+// the emit reads instead of searching again (collect_few_hits).
+template <class PosJ>
+__device__ __forceinline__ int count_few(const StructMeta& M, const DGN_LDS u32x4* fx, const DGN_LDS f64x4* offt,
+                                         PosJ&& posj, int li, double rc2, double eps, DGN_LDS uint64_t* mask_words) {
+    const int lane = lane_id();
+    const int natoms = M.natoms;
+    const u32x4 fq = fx[li];
+    const float lo32 = M.lo32, hi32 = M.hi32;
+    float h[3];
+    few_halfwidths(M, h);
+    const bool skip_self = 0.0 < eps;
+    int m = 0;
+#pragma nounroll
+    for (int base = 0; base < natoms; base += kWave) {
+        const int j = base + lane;
+        const bool valid = j < natoms;
+        const FewLane r = few_lane(h, fq, fx[valid ? j : li]);
+        const uint32_t okm = valid ? r.ok : 0u;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const bool allowed = few_combo_ok(okm, c) && !(c == 0 && skip_self && j == li);
+            if (!ballot(allowed)) {  // wave-uniform: no lane has this combination
+                if (mask_words && lane == 0) mask_words[c] = 0;
+                continue;
+            }
+            const float d2 = few_d2(M, r, c);
+            bool hit = allowed && d2 < lo32;
+            if (allowed && !hit && d2 <= hi32) {
+                int n[3];
+                few_image(r, c, n);
+                double q[3];
+                posj(li, q);
+                hit = exact_at_n(M, offt, posj, j, q, n, true) < rc2;
+            }
+            const uint64_t bal = ballot(hit);
+            if (mask_words && lane == 0) mask_words[c] = bal;
+            m += __popcll(bal);
+        }
+    }
+    return m;
+}
+
+// Hit collection on a staged `few` structure (emit / Betti): the combinations at or below hi32
+// queue in the per-wave LDS ring as (c << 16 | j) and are exact-tested 64 at a time.
+template <class Visit>
+__device__ __forceinline__ void search_staged_few(const StructMeta& M, const StageView st, const double q[3], int li,
+                                                  double rc2, double eps, DGN_LDS uint32_t* ring, Visit&& visit) {
+    const int lane = lane_id();
+    const int natoms = M.natoms;
+    const u32x4 fq = st.fx[li];
+    const float hi32 = M.hi32;
+    float h[3];
+    few_halfwidths(M, h);
+    auto posj = [&](int jj, double p[3]) __attribute__((always_inline)) {
+        p[0] = st.x[jj];
+        p[1] = st.y[jj];
+        p[2] = st.z[jj];
+    };
+    int head = 0, cnt = 0;
+    auto flush = [&](int take) {
+        wave_lds_sync();
+        const bool valid = lane < take;
+        const uint32_t e = valid ? ring[(head + lane) & (kRing - 1)] : (uint32_t)li;
+        const int j = (int)(e & 0xffffu), c = (int)(e >> 16);
+        const FewLane r = few_lane(h, fq, st.fx[j]);
+        int n[3];
+        few_image(r, c, n);
+        const double d2 = exact_at_n(M, st.offt, posj, j, q, n, valid);
+        bool hit = valid && d2 < rc2;                 // RadiusResultSet: strict
+        if (hit && j == li) hit = !(sqrt(d2) < eps);  // self skip (neighbor_list.cpp:47)
+        visit(hit, j, n[0], n[1], n[2], d2);
+        head = (head + take) & (kRing - 1);
+        cnt -= take;
+        wave_lds_sync();
+    };
+    for (int base = 0; base < natoms; base += kWave) {
+        const int j = base + lane;
+        const bool valid = j < natoms;
+        const FewLane r = few_lane(h, fq, st.fx[valid ? j : li]);
+        const uint32_t okm = valid ? r.ok : 0u;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const bool allowed = few_combo_ok(okm, c);
+            if (!ballot(allowed)) continue;
+            const bool pass = allowed && few_d2(M, r, c) <= hi32;
+            const uint64_t bal = ballot(pass);
+            if (pass) ring[(head + cnt + mask_prefix(bal)) & (kRing - 1)] = ((uint32_t)c << 16) | (uint32_t)j;
+            cnt += __popcll(bal);
+            if (cnt >= kWave) flush(kWave);
+        }
+    }
+    while (cnt > 0) flush(cnt < kWave ? cnt : kWave);
 }
 
 // (2) cell list (structures above kStage atoms, one image per axis)
@@ -736,6 +931,8 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
     if (M.one && P.staged) {
         if (mask) search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, load_mask(mask, M.natoms), visit);
         else search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, ApproxOne{P.st, M, li, g.rc2}, visit);
+    } else if (M.few && P.staged) {
+        search_staged_few(M, P.st, q, li, g.rc2, g.eps, ring, visit);
     } else if (M.one && M.cells) {
         search_cells(g, M, b, q, li, visit);
     } else {
@@ -909,6 +1106,16 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
             if (M.one && P.staged) {
                 m = count_staged_one(M, P.st, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr);
                 nw = mask_out ? (M.natoms + 63) / 64 : 0;
+            } else if (M.few && P.staged) {
+                m = count_few(
+                    M, P.st.fx, P.st.offt,
+                    [&](int jj, double p[3]) __attribute__((always_inline)) {
+                        p[0] = P.st.x[jj];
+                        p[1] = P.st.y[jj];
+                        p[2] = P.st.z[jj];
+                    },
+                    li, g.rc2, g.eps, (mask_out && M.natoms <= kWave) ? lds(mask_s[t]) : nullptr);
+                nw = (mask_out && M.natoms <= kWave) ? kFewMaskWords : 0;
             } else {
                 double q[3];
                 P.get(li, q);
@@ -1546,19 +1753,32 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         // count pass's hits are evaluated)
         int m = 0;
         bool fast = false;
-        const DGN_LDS uint64_t* mk = (g.mask && M.one && P.staged) ? mask_s + t * nwm : nullptr;
+        // (`few` structures of <= 64 atoms: a hit word per image combination, collect_few_hits)
+        const bool few_mask = M.few && M.natoms <= kWave && nwm >= kFewMaskWords;
+        const DGN_LDS uint64_t* mk = (g.mask && (M.one || few_mask) && P.staged) ? mask_s + t * nwm : nullptr;
         if (mk) {
             // fast path: at most 64 hits, one lane each, straight from the count pass's mask
-            const int mh = collect_mask_hits(mk, M.natoms, lds(ring[w]));
+            const int mh = M.one ? collect_mask_hits(mk, M.natoms, lds(ring[w])) : collect_few_hits(mk, lds(ring[w]));
             if (mh <= kWave) {
                 fast = true;
                 m = mh;
                 bool ok = true;
                 if (lane < m) {
-                    const int j = (int)ring[w][lane];
+                    const uint32_t e = ring[w][lane];
+                    const int j = (int)(e & 0xffffu);
                     int n[3];
-                    bool inr;
-                    const double d2 = exact_one(M, P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    bool inr = true;
+                    double d2;
+                    if (M.one) {
+                        d2 = exact_one(M, P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
+                    } else {
+                        float h[3];
+                        few_halfwidths(M, h);
+                        few_image(few_lane(h, P.st.fx[li], P.st.fx[j]), (int)(e >> 16), n);
+                        d2 = exact_at_n(
+                            M, P.st.offt,
+                            [&](int jj, double p[3]) __attribute__((always_inline)) { P.get(jj, p); }, j, q, n, true);
+                    }
                     ok = inr && d2 < g.rc2;
                     kd[lane] = sqrt(d2);  // neighbor_list.cpp:53
                     kj[lane] = pack_jimg(j, n[0], n[1], n[2]);
@@ -1874,7 +2094,9 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
                           const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist, double* disp,
                           void* rbf, const RbfSpec& rs, uint32_t* error_flag, EmitKeys gk) {
     const int64_t nt = graph_blocks(g.num_atoms, g.qa);
-    const int nwm = (stage + 63) / 64;
+    // mask words per atom staged by the emit: the atom tiles of the largest structure, and at least
+    // kFewMaskWords when every structure has <= 64 atoms (a `few` structure's combination words)
+    const int nwm = stage <= kWave ? kFewMaskWords : (stage + 63) / 64;
     const int K = g.kmax < (uint64_t)0x7fffffff ? (int)g.kmax : 0x7fffffff;
     const EmitLayout ly = emit_layout(stage, CAP, STREAM, K, rs.dtype ? rs.nbins : 0, rs.dtype == 2 ? 8 : 4, nwm);
     const int fused = STREAM && rs.dtype != 0 && rbf ? 1 : 0;

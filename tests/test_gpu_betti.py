@@ -98,6 +98,20 @@ def test_mixed_one_image_and_general_tiles(ctx):
         np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
 
 
+def test_few_image_cells(ctx):
+    # cells between rc and 2 rc wide (the `few` staged search builds the local clouds): triclinic
+    # and axis-aligned, atoms partly outside the cell
+    from test_gpu_graph import few_image_batch
+    batch = few_image_batch(5, B=8, nmax=36)
+    f, c = ctx.host_betti(batch, 5.0)
+    off = batch["atom_offset"]
+    for s in range(len(off) - 1):
+        sl = slice(off[s], off[s + 1])
+        fo, co = O.structure_betti(batch["lattice"][s], batch["positions"][sl], batch["species"][sl], 5.0)
+        assert np.array_equal(c[sl], co)
+        np.testing.assert_allclose(f[sl], fo, rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
 def test_isolated_atom(ctx):
     one = {"lattice": np.eye(3)[None] * 30.0, "positions": np.array([[1.0, 1.0, 1.0], [15.0, 15.0, 15.0]]),
            "species": np.array([0, 1], np.int32), "atom_offset": np.array([0, 2], np.int64)}

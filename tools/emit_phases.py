@@ -1,5 +1,6 @@
 """Diagnostics: per-phase s_memtime cycles of the graph emit (libdgn built with -DDGN_EMIT_PHASES).
-    DGN_LIB=defect-gnn-cpp_amd/lib/libdgn_diag_ph.so python tools/emit_phases.py [reps]"""
+    DGN_LIB=defect-gnn-cpp_amd/lib/libdgn_diag_ph.so python tools/emit_phases.py [reps] [kind m B]
+    (default fcc 4 8192 = config 4; sc 4 1024 = config 2)"""
 import ctypes as C
 import os
 import sys
@@ -12,7 +13,9 @@ from dgn import abi  # noqa: E402
 NAMES = ["setup", "stage+loop", "hits+exact", "rank+put", "rbf", "-", "-", "-"]
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 ctx = dgn.Context(0)
-host = dgn.synth_batch("fcc", 4, 8192)
+kind = sys.argv[2] if len(sys.argv) > 2 else "fcc"
+m_, B_ = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (4, 8192)
+host = dgn.synth_batch(kind, m_, B_)
 batch = {k: torch.from_numpy(v).cuda() for k, v in host.items()}
 gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F32)
 E = ctx.dev_graph_count(batch, gp)
