@@ -141,32 +141,31 @@ def main():
         rc["wait_frac"] = round(wide["SQ_WAIT_ANY"] / wide["SQ_WAVE_CYCLES"], 3)
     json.dump(rc, open(os.path.join(HERE, "r04_rc10_wide.json"), "w"), indent=1)
 
-    # BASELINE configs 2 and 5 (tools/side_graph.py 20: config2, config5 f32, then f64), per dispatch
+    # BASELINE configs 2 and 5 (tools/side_graph.py 20 runs config2, config5 with the f32 RBF, then
+    # both with f64, one after the other): dispatches in time order, a new phase whenever the
+    # one-image count kernel's grid changes (config 2: 2,048 blocks, config 5: 1,024)
     tr = glob.glob(os.path.join(D, "side", "**", "*kernel_trace.csv"), recursive=True)
     if tr:
         rs = sorted(csv.DictReader(open(tr[0])), key=lambda r: int(r["Start_Timestamp"]))
-        acc = collections.defaultdict(list)
+        phases, cur, grid = [], None, None
         for r in rs:
             if "dgn::" not in r["Kernel_Name"]:
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("dgn::", "")
-            acc[(name, int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-        out = {"config2": {"f32": {}, "f64": {}}, "config5": {"f32": {}, "f64": {}}}
-        big = max(g for (_, g) in acc)
-        for (name, grid), v in acc.items():
-            cfg = "config2" if grid == big or (name in ("prep_atoms_kernel",) and grid > 1024) or \
-                (name == "prep_meta_kernel" and grid == 1024) else "config5"
-            h = len(v) // 2
-            for half, vals in (("f32", v[:h]), ("f64", v[h:])):
-                vals = sorted(vals)
-                if vals:
-                    out[cfg][half][name] = round(vals[len(vals) // 2], 2)
-        for cfg in out:
-            for dt in out[cfg]:
-                out[cfg][dt]["path_us"] = round(sum(x for k, x in out[cfg][dt].items() if k != "path_us"), 1)
-        out["note"] = ("median kernel durations (us) per dispatch, rocprofv3 --kernel-trace; config 2 = 1,024 SC-64 cells "
-                       "(grid 2,048 blocks), config 5 = one 4,096-atom SC supercell (1,024 blocks of 4 atoms); "
-                       "graph rc 5, K 20, 50-bin RBF")
+            if name == "graph_count_one_kernel" and r["Grid_Size_X"] != grid:
+                grid = r["Grid_Size_X"]
+                cur = collections.defaultdict(list)
+                phases.append(cur)
+            if cur is not None:
+                cur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        out = {"config2": {}, "config5": {}}
+        for (cfg, dt), ph in zip((("config2", "f32"), ("config5", "f32"), ("config2", "f64"), ("config5", "f64")), phases):
+            med = {k: round(sorted(v)[len(v) // 2], 2) for k, v in ph.items()}
+            med["path_us"] = round(sum(med.values()), 1)
+            out[cfg][dt] = med
+        out["note"] = ("median kernel durations (us) per dispatch, rocprofv3 --kernel-trace of tools/side_graph.py 20; "
+                       "config 2 = 1,024 SC-64 cells (grid 2,048 blocks; cells narrower than 2 rc: the few-image search), "
+                       "config 5 = one 4,096-atom SC supercell (1,024 blocks of 4 atoms; cell list); graph rc 5, K 20, 50-bin RBF")
         json.dump(out, open(os.path.join(HERE, "r04_side_graph.json"), "w"), indent=1)
 
 
