@@ -475,9 +475,12 @@ __device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq,
 // lattice and the window [lo32, hi32] = rc^2 -+ band32 come from prep_meta_kernel (derivation
 // there).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// skip_self: eps > 0, so the query's own image (n = 0, d2 = 0) is skipped (neighbor_list.cpp:47); its
+// other images are beyond 2 rc here
 template <class PosJ>
 __device__ __forceinline__ int count_one_image(const StructMeta& M, const DGN_LDS u32x4* fx, const DGN_LDS f64x4* offt,
-                                               PosJ&& posj, int li, double rc2, DGN_LDS uint64_t* mask_words) {
+                                               PosJ&& posj, int li, double rc2, DGN_LDS uint64_t* mask_words,
+                                               bool skip_self) {
     const int lane = lane_id();
     const int natoms = M.natoms;
     const u32x4 fq = fx[li];
@@ -503,7 +506,7 @@ __device__ __forceinline__ int count_one_image(const StructMeta& M, const DGN_LD
             dz = __builtin_elementwise_fma(u2, (f32x2)Lf[8], __builtin_elementwise_fma(u1, (f32x2)Lf[5], u0 * Lf[2]));
         }
         const f32x2 d2 = __builtin_elementwise_fma(dx, dx, __builtin_elementwise_fma(dy, dy, dz * dz));
-        const bool ok0 = j0 < natoms && j0 != li, ok1 = j1 < natoms && j1 != li;
+        const bool ok0 = j0 < natoms && !(skip_self && j0 == li), ok1 = j1 < natoms && !(skip_self && j1 == li);
         bool hit0 = ok0 && d2.x < lo32, hit1 = ok1 && d2.y < lo32;
         // borderline: the exact reference arithmetic decides (the query position is only read
         // here, a few times per thousand queries)
@@ -533,7 +536,7 @@ __device__ __forceinline__ int count_one_image(const StructMeta& M, const DGN_LD
     return m;
 }
 __device__ __forceinline__ int count_staged_one(const StructMeta& M, const StageView st, int li, double rc2,
-                                                DGN_LDS uint64_t* mask_words) {
+                                                DGN_LDS uint64_t* mask_words, bool skip_self) {
     return count_one_image(
         M, st.fx, st.offt,
         [&](int jj, double p[3]) __attribute__((always_inline)) {
@@ -541,7 +544,7 @@ __device__ __forceinline__ int count_staged_one(const StructMeta& M, const Stage
             p[1] = st.y[jj];
             p[2] = st.z[jj];
         },
-        li, rc2, mask_words);
+        li, rc2, mask_words, skip_self);
 }
 
 // Hit collection on a staged one-image structure (emit / Betti): `produce(base, lane, fq) -> bool`
@@ -589,9 +592,10 @@ struct ApproxOne {
     int li;
     __device__ __forceinline__ bool operator()(int base, int lane, const u32x4 fq) const {
         const int j = base + lane;
-        return j != li && approx_d2(M, fq, st.fx[j]) <= rc2_ + M.band;
+        return (j != li || keep_self) && approx_d2(M, fq, st.fx[j]) <= rc2_ + M.band;
     }
     double rc2_;
+    bool keep_self;  // eps <= 0: the self image (d = 0) is not skipped by the reference either
 };
 // the count pass's exact hits of this query (one bit per atom): lane t holds word t (one
 // coalesced load per query), each tile reads its word with v_readlane
@@ -942,7 +946,7 @@ __device__ __forceinline__ void search(const GraphLaunch& g, const StructMeta& M
                                        const DGN_LDS uint64_t* mask, Visit&& visit) {
     if (M.one && P.staged) {
         if (mask) search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, load_mask(mask, M.natoms), visit);
-        else search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, ApproxOne{P.st, M, li, g.rc2}, visit);
+        else search_staged_one(M, P.st, q, li, g.rc2, g.eps, ring, ApproxOne{P.st, M, li, g.rc2, !(0.0 < g.eps)}, visit);
     } else if (M.few && P.staged) {
         search_staged_few(M, P.st, q, li, g.rc2, g.eps, ring, visit);
     } else if (M.one && M.cells) {
@@ -1086,7 +1090,7 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
                 p[1] = gp[3 * jj + 1];
                 p[2] = gp[3 * jj + 2];
             },
-            li, g.rc2, lds(mask_s[t]));
+            li, g.rc2, lds(mask_s[t]), 0.0 < g.eps);
         if (lane == 0) {
             cnt_s[t] = (int32_t)m;
             nw_s[t] = (M.natoms + 63) / 64;
@@ -1116,7 +1120,7 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
             const int li = (int)(gi - M.first);
             int m = 0, nw = 0;
             if (M.one && P.staged) {
-                m = count_staged_one(M, P.st, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr);
+                m = count_staged_one(M, P.st, li, g.rc2, mask_out ? lds(mask_s[t]) : nullptr, 0.0 < g.eps);
                 nw = mask_out ? (M.natoms + 63) / 64 : 0;
             } else if (M.few && P.staged) {
                 m = count_few(

@@ -15,13 +15,13 @@ pytestmark = pytest.mark.gpu
 RBF_RTOL = 1e-6  # north_star: RBF/distance floats within 1e-6 relative
 
 
-def oracle_batch_csr(batch, rc, k):
+def oracle_batch_csr(batch, rc, k, epsilon=1e-10):
     rp_all, col_all, dist_all, disp_all = [np.zeros(1, np.int64)], [], [], []
     off = batch["atom_offset"]
     base = 0
     for s in range(len(off) - 1):
         a, b = off[s], off[s + 1]
-        nl = O.neighbor_list(batch["lattice"][s], batch["positions"][a:b], rc, k)
+        nl = O.neighbor_list(batch["lattice"][s], batch["positions"][a:b], rc, k, epsilon=epsilon)
         rp_all.append(nl["row_ptr"][1:] + base)
         base += nl["row_ptr"][-1]
         col_all.append(nl["col"])
@@ -168,6 +168,28 @@ def test_few_image_cells(ctx, seed, k):
     assert np.array_equal(g["col"], col)
     assert np.array_equal(g["dist"], dist)
     assert np.array_equal(g["disp"], disp)
+
+
+@pytest.mark.parametrize("eps", [0.0, 1e-10, 5.0])
+def test_self_image_epsilon(ctx, eps):
+    """NeighborList's epsilon skips only images of the query atom closer than eps
+    (neighbor_list.cpp:47): eps = 0 keeps the atom itself at distance 0, eps = 5 also drops its
+    periodic images inside a 4.64 A cell. One-image (FCC-256), few-image (SC-64) and general
+    (SC-8, L < rc) structures in one batch, CSR bit-exact vs the oracle at the same epsilon."""
+    parts = [dgn.synth_batch("fcc", 4, 1), dgn.synth_batch("sc", 4, 2), dgn.synth_batch("sc", 2, 2)]
+    batch = {k: np.concatenate([x[k] for x in parts]) for k in ("lattice", "positions", "species")}
+    sizes = np.concatenate([np.diff(x["atom_offset"]) for x in parts])
+    batch["atom_offset"] = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    p = abi.graph_params(r_cutoff=5.0, max_neighbors=None, epsilon=eps, rbf_cutoff=5.0, rbf_dr=0.1,
+                         write_displacement=True)
+    g = ctx.host_graph(batch, p)
+    rp, col, dist, disp = oracle_batch_csr(batch, 5.0, None, epsilon=eps)
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
+    if eps == 0.0:
+        assert (g["dist"] == 0.0).sum() == len(batch["positions"])  # every atom lists itself once
 
 
 @pytest.mark.parametrize("layout", [0, 1])
