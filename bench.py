@@ -318,6 +318,15 @@ def side_lines(dgn, abi, ctx, dev, args, torch):
     out["betti_rc10"] = {"workload": "32 x FCC-256 (8,192 complexes of ~340 points), Betti-0/1/2 at rc 10",
                          "structures_per_s": round(sh.B / dt, 2), "complexes_per_s": round(sh.A / dt, 1),
                          "ms": round(dt * 1e3, 2), "betti_vr_ms": kt.get("betti_vr")}
+    del sh
+    # the same at a 128-structure batch (32,768 complexes, ~7 per resident wave): the steady-state
+    # rate; at 32 structures each resident wave reduces one or two complexes and the last ones idle
+    sh = Shard(dgn, abi, "fcc", 4, 128, 0, dev)
+    sh.alloc_betti()
+    dt, kt = timed(sh, gp, 10.0, True, graph=False)
+    out["betti_rc10_b128"] = {"workload": "128 x FCC-256 (32,768 complexes of ~340 points), Betti-0/1/2 at rc 10",
+                              "structures_per_s": round(sh.B / dt, 2), "complexes_per_s": round(sh.A / dt, 1),
+                              "ms": round(dt * 1e3, 2), "betti_vr_ms": kt.get("betti_vr")}
     return out
 
 
