@@ -1069,34 +1069,50 @@ __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN
     const int64_t tile = blockIdx.x;
     const int64_t g0 = tile * g.qa;
     const int64_t g1 = g0 + g.qa < g.num_atoms ? g0 + g.qa : g.num_atoms;
-    // every structure of the tile staged and one-image? (wave-uniform: metadata in SGPRs)
-    bool one = true;
+    // every structure of the tile staged and one-image or few-image? (wave-uniform: metadata in
+    // SGPRs)
+    bool one = true, all_one = true;
     for (int32_t b = uni_i32(g.atom_struct[g0]), bl = uni_i32(g.atom_struct[g1 - 1]); b <= bl && one; ++b) {
         const StructMeta M = load_meta_uniform(g.meta + b);
-        one = M.natoms == 0 || (M.one && M.natoms <= kStage);
+        one = M.natoms == 0 || ((M.one || M.few) && M.natoms <= kStage);
+        all_one = all_one && (M.natoms == 0 || M.one);
     }
     if (threadIdx.x == 0) defer[tile] = one ? 0 : 1;  // every tile's flag is written: no memset
     if (!one) return;
     // stage view without positions (for_block_atoms<false> stores fx and the offset table only)
     const StageView st{nullptr, nullptr, nullptr, lds(fx_s), reinterpret_cast<DGN_LDS f64x4*>(lds(offt_s)), kStage};
     CountAcc acc;
-    for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t) __attribute__((always_inline)) {
+    // per query atom: M.one -> the one-image count, else the few-image count; the all-one-image
+    // tiles (config 4) take a loop of their own, so their code is laid out as without the few path
+    auto per_atom = [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, bool only_one) __attribute__((always_inline)) {
         const int li = (int)(gi - M.first);
         const double* gp = P.gpos;
-        const int m = count_one_image(
-            M, st.fx, st.offt,
-            [&](int jj, double p[3]) __attribute__((always_inline)) {
-                p[0] = gp[3 * jj];
-                p[1] = gp[3 * jj + 1];
-                p[2] = gp[3 * jj + 2];
-            },
-            li, g.rc2, lds(mask_s[t]), 0.0 < g.eps);
+        auto posj = [&](int jj, double p[3]) __attribute__((always_inline)) {
+            p[0] = gp[3 * jj];
+            p[1] = gp[3 * jj + 1];
+            p[2] = gp[3 * jj + 2];
+        };
+        int m, nw;
+        if (only_one || M.one) {
+            m = count_one_image(M, st.fx, st.offt, posj, li, g.rc2, lds(mask_s[t]), 0.0 < g.eps);
+            nw = (M.natoms + 63) / 64;
+        } else {
+            const bool words = M.natoms <= kWave;  // a hit word per image combination (collect_few_hits)
+            m = count_few(M, st.fx, st.offt, posj, li, g.rc2, g.eps, words ? lds(mask_s[t]) : nullptr);
+            nw = words ? kFewMaskWords : 0;
+        }
         if (lane == 0) {
             cnt_s[t] = (int32_t)m;
-            nw_s[t] = (M.natoms + 63) / 64;
+            nw_s[t] = nw;
         }
         acc.add(m, M.natoms, g.kmax);
-    });
+    };
+    if (all_one)
+        for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t)
+                                   __attribute__((always_inline)) { per_atom(M, P, gi, t, true); });
+    else
+        for_block_atoms<false>(g, st, 0, g.num_atoms, tile, g.qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t)
+                                   __attribute__((always_inline)) { per_atom(M, P, gi, t, false); });
     count_tile_store(g, tile, acc, out, counts, block_sums, block_aux, mask_out);
 }
 
