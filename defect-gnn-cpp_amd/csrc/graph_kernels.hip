@@ -975,9 +975,9 @@ __device__ __forceinline__ int64_t mask_index(int64_t gi, int wd, int qa) {
 // size). No atomics on the data. For staged one-image structures it also records each query's
 // exact hits as a bit per atom (word-major per tile, mask_index) so the emit and Betti passes
 // skip the search. Two kernels (launch_graph_count):
-//   1a graph_count_one_kernel, every tile: tiles whose structures are all staged one-image ones
-//      (cells wider than 2 rc, <= kStage atoms: config 4's FCC-256 at 5 A) are counted here; any
-//      other tile is flagged and left alone;
+//   1a graph_count_one_kernel, every tile: tiles whose structures are all staged one-image or
+//      few-image ones (cells wider than rc, <= kStage atoms: config 4's FCC-256 at 5 A, config 2's
+//      SC-64) are counted here; any other tile is flagged and left alone;
 //   1b graph_count_kernel over the flagged tiles (every search strategy).
 // 1a stages only the fixed-point coordinates (16 B per atom) and the image-offset table; the rare
 // borderline exact test reads positions from global memory. Without the general / cell-list
