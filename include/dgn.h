@@ -115,7 +115,9 @@ enum { DGN_NONE = 0, DGN_F32 = 1, DGN_F64 = 2 };
 typedef struct {
     double r_cutoff;        /* NeighborList r_cutoff (reference default 10.0)           */
     uint64_t max_neighbors; /* reference default 20; UINT64_MAX = unlimited           */
-    double epsilon;         /* self-image skip threshold (1e-10)                      */
+    double epsilon;         /* self-image skip threshold (1e-10): an image of the query atom
+                               closer than epsilon is skipped (neighbor_list.cpp:47); epsilon <= 0
+                               keeps the atom itself at distance 0, as the reference does */
     double rbf_cutoff;      /* CrystalGraph r_cutoff for the RBF (default 10.0)       */
     double rbf_dr;          /* CrystalGraph dr (default 0.1)                          */
     int32_t rbf_dtype;      /* DGN_F32 (default), DGN_F64, DGN_NONE                    */
