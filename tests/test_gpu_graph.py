@@ -133,18 +133,19 @@ def test_mixed_one_image_and_general_tiles(ctx, npairs):
     assert np.array_equal(g["disp"], disp)
 
 
-def few_image_batch(seed, B=24, rc=5.0, nmax=90):
+def few_image_batch(seed, B=24, rc=5.0, nmax=90, hlo=0.5, hhi=0.98):
     """Cells whose perpendicular widths lie between rc and 2 rc (max H_k in (0.5, 1): at most two
     images per axis reach rc, the `few` staged search), triclinic and axis-aligned, 5..nmax atoms
     with fractional coordinates in [-0.2, 1.2) (atoms outside the cell: images n = +-2)."""
     rng = np.random.default_rng(seed)
     lat, pos, sizes = [], [], []
     while len(lat) < B:
-        L = np.diag(rng.uniform(1.05, 1.9, 3) * rc) + np.triu(rng.uniform(-0.35, 0.35, (3, 3)) * rc, 1)
+        lo = 1.0 / hhi if hhi > 0.98 else 1.05  # cells just wider than rc when hhi is near 1
+        L = np.diag(rng.uniform(lo, 1.9, 3) * rc) + np.triu(rng.uniform(-0.35, 0.35, (3, 3)) * rc, 1)
         if len(lat) % 3 == 0:
             L = np.diag(np.diag(L))
         H = rc * np.linalg.norm(np.linalg.inv(L), axis=0)
-        if not (0.5 < H.max() < 0.98) or np.linalg.norm(L, axis=1).min() < rc:
+        if not (hlo < H.max() < hhi) or np.linalg.norm(L, axis=1).min() < rc:
             continue
         n = int(rng.integers(5, nmax))
         lat.append(L)
@@ -155,12 +156,14 @@ def few_image_batch(seed, B=24, rc=5.0, nmax=90):
             "atom_offset": np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)}
 
 
-@pytest.mark.parametrize("seed,k", [(1, 20), (2, None), (3, 7)])
-def test_few_image_cells(ctx, seed, k):
+@pytest.mark.parametrize("seed,k,hlo,hhi", [(1, 20, 0.5, 0.98), (2, None, 0.5, 0.98), (3, 7, 0.5, 0.98),
+                                             (4, None, 0.95, 0.9995)])
+def test_few_image_cells(ctx, seed, k, hlo, hhi):
     """Cells narrower than 2 rc but wider than rc (search_staged_few / count_few: up to 2^3 images
     of an atom decided in f32, borderline ones exactly): CSR, distances and displacements bit-exact
-    vs the oracle's (2 nref + 1)^3 image scan."""
-    batch = few_image_batch(seed)
+    vs the oracle's (2 nref + 1)^3 image scan; the last case has a width within 0.05 % of rc on some
+    axis (two images per axis for nearly every pair)."""
+    batch = few_image_batch(seed, hlo=hlo, hhi=hhi)
     p = abi.graph_params(r_cutoff=5.0, max_neighbors=k, rbf_cutoff=5.0, rbf_dr=0.1, write_displacement=True)
     g = ctx.host_graph(batch, p)
     rp, col, dist, disp = oracle_batch_csr(batch, 5.0, k)
