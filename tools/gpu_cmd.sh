@@ -1,5 +1,10 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_graph.py -k "few or epsilon" > gpurun_out/t_few2.log 2>&1 || { tail -30 gpurun_out/t_few2.log; exit 1; }
-tail -3 gpurun_out/t_few2.log
+mkdir -p gpurun_out/ab_w
+for r in 1 2; do
+  for t in base w4 w6; do
+    lib=defect-gnn-cpp_amd/lib/libdgn.so; [ $t != base ] && lib=defect-gnn-cpp_amd/lib/libdgn_$t.so
+    DGN_LIB=$lib timeout -k 10 150 python -u tools/betti_rc10.py 128 2 > gpurun_out/ab_w/${t}_$r.log 2>&1 || exit 1
+    echo "$t $(grep -o '= [0-9.]* structures/s' gpurun_out/ab_w/${t}_$r.log | tail -1)"
+  done
+done
