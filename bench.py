@@ -310,6 +310,15 @@ def side_lines(dgn, abi, ctx, dev, args, torch):
                       "graph_ms": round(dt * 1e3, 4), "graph_path_kernels_ms": round(gk, 4),
                       "graph_path_hbm_frac": round(graph_bytes_8d(sh.A, 1, sh.E, nb, 4) / (gk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                       if gk else None, "betti_ms": round(dt2 * 1e3, 4)}
+    # the cell-list Betti search (> 512 atoms): every atom of the timed supercell vs the oracle
+    import numpy as np
+    import oracle_py as O
+    fo, co = O.structure_betti(sh.host["lattice"][0], sh.host["positions"], sh.host["species"], 5.0)
+    gf, gc = sh.out["feat"].cpu().numpy(), sh.out["counts"].cpu().numpy()
+    rel = np.abs(gf - fo) / np.maximum(np.abs(fo), 1e-12)
+    out["config5"]["betti_parity"] = {"atoms_checked": int(sh.A), "counts_exact": bool(np.array_equal(gc, co)),
+                                      "feat_within_1e-6": bool(np.all((rel <= 1e-6) | (np.abs(gf - fo) <= 1e-12))),
+                                      "checker": "oracle structure_betti (pinned to verbatim Ripser, cellist.npz)"}
     del sh
     # the reference's default Betti cutoff, 10 A (~340-point complexes, wide kernel)
     sh = Shard(dgn, abi, "fcc", 4, 32, 0, dev)

@@ -3,6 +3,7 @@
     python tests/golden/make_golden.py          # everything
     python tests/golden/make_golden.py rc10     # only the 10 A fixtures (rc10.npz)
     python tests/golden/make_golden.py rc16     # only the 16 A fixtures (rc16.npz; ~45 min, ~34 GB)
+    python tests/golden/make_golden.py cellist  # only the > 512-atom fixtures (cellist.npz)
 
 Inputs: the reference's own POSCAR files (/root/reference/web/public/data/structures/*.vasp,
 parsed here as data) and synthetic SC cells from the bit-reproducible generator.
@@ -105,10 +106,55 @@ def rc16_fixtures():
         np.savez_compressed(os.path.join(OUT, "rc16.npz"), **out)
 
 
+def triclinic_cell_688():
+    """A 688-atom triclinic cell (above the 512-atom cell-list threshold of the Betti search): a
+    jittered 8 x 9 x 9 grid in fractional coordinates of a sheared cell at 0.08 atoms/A^3, every
+    37th atom moved one cell out (images n = +-1 in the reference's scan), and a 40-atom pocket
+    around site 100 so that the local complexes span every tier (34..88 points at rc 5)."""
+    rng = np.random.default_rng(2025)
+    g = (8, 9, 9)
+    n0 = int(np.prod(g))
+    lat = np.array([[20.0, 0, 0], [3.5, 19.0, 0], [-2.5, 4.0, 21.0]]) * ((n0 / 0.08) / (20 * 19 * 21)) ** (1 / 3)
+    idx = np.stack(np.meshgrid(*[np.arange(k) for k in g], indexing="ij"), -1).reshape(-1, 3)
+    frac = (idx + 0.5 + rng.uniform(-0.3, 0.3, (n0, 3))) / np.array(g)
+    frac[::37] += rng.choice([-1, 1], (len(frac[::37]), 3))
+    pocket = frac[100] @ lat + rng.normal(0, 1.2, (40, 3))
+    pos = np.vstack([frac @ lat, pocket])
+    return lat, pos, (np.arange(pos.shape[0]) % 3).astype(np.int32)
+
+
+CELLIST_SC_STRIDE = 8
+
+
+def cellist_fixtures():
+    """(vi) Structures above 512 atoms, where the Betti pass's neighbour search uses the cell list
+    (betti_features.cpp:103-119 over neighbor_list.cpp:27-66): verbatim-Ripser counts + 35
+    statistics of
+      * config 5's SC-4096 supercell (synthetic generator, sc m = 16) at rc 5, every 8th atom;
+      * the 688-atom triclinic cell above (positions stored) at rc 5, every atom.
+    Written to cellist.npz."""
+    out = {}
+    bt = synth.make_batch("sc", 16, 1)
+    f, c = O.ref_structure_betti(bt["lattice"][0], bt["positions"], bt["species"], 5.0, omp_threads=8,
+                                 ripser_threads=1)
+    out["sc4096/atoms"] = np.arange(0, bt["positions"].shape[0], CELLIST_SC_STRIDE, dtype=np.int32)
+    out["sc4096/features"] = f[::CELLIST_SC_STRIDE]
+    out["sc4096/counts"] = c[::CELLIST_SC_STRIDE]
+    lat, pos, sp = triclinic_cell_688()
+    f, c = betti_ref(lat, pos, sp, 5.0)
+    out["tri688/lattice"], out["tri688/positions"], out["tri688/species"] = lat, pos, sp
+    out["tri688/features"], out["tri688/counts"] = f, c
+    np.savez_compressed(os.path.join(OUT, "cellist.npz"), **out)
+    print("cellist: sc4096", bt["positions"].shape[0], "atoms; tri688", pos.shape[0], "atoms")
+
+
 def main():
     assert O.ref_available(), "build oracle/_ref first (make -C oracle)"
     if sys.argv[1:] == ["rc10"]:
         rc10_fixtures()
+        return
+    if sys.argv[1:] == ["cellist"]:
+        cellist_fixtures()
         return
     if sys.argv[1:] == ["rc16"]:
         rc16_fixtures()
@@ -194,6 +240,7 @@ def main():
         kat[f"{name}/n_inf0"] = np.int32(pr["n_inf0"])
     np.savez_compressed(os.path.join(OUT, "kat.npz"), **kat)
     rc10_fixtures()
+    cellist_fixtures()
     for f in sorted(glob.glob(os.path.join(OUT, "*.npz"))):
         print(f, os.path.getsize(f), "bytes")
 

@@ -143,3 +143,14 @@ def test_restated_reduction_vs_verbatim_ripser_random():
         for d in ("dim0", "dim1", "dim2"):
             assert np.array_equal(a[d], b[d]), (t, d)
         assert a["n_inf0"] == b["n_inf0"]
+
+
+def test_cellist_fixture_sc4096():
+    """The oracle over config 5's SC-4096 supercell vs verbatim Ripser (every 8th atom of
+    cellist.npz): pins the checker the > 512-atom GPU tests compare against."""
+    fx = np.load(os.path.join(GOLDEN, "cellist.npz"))
+    bt = synth.make_batch("sc", 16, 1)
+    f, c = O.structure_betti(bt["lattice"][0], bt["positions"], bt["species"], 5.0)
+    a = fx["sc4096/atoms"]
+    assert np.array_equal(c[a], fx["sc4096/counts"])
+    np.testing.assert_allclose(f[a], fx["sc4096/features"], rtol=1e-12, atol=1e-12)

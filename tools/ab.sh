@@ -9,7 +9,8 @@ export TMPDIR=/tmp
 for r in $(seq 1 $R); do
   for tag in "$@"; do
     lib=defect-gnn-cpp_amd/lib/libdgn.so; [ "$tag" != base ] && lib=defect-gnn-cpp_amd/lib/libdgn_$tag.so
-    DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-alt-rbf \
+    # shellcheck disable=SC2086  # BENCH_ARGS (optional): another workload, e.g. "--kind sc --betti-rc 4.5"
+    DGN_LIB=$lib timeout -k 10 180 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side --no-alt-rbf ${BENCH_ARGS:-} \
         > "$OUT/${tag}_$r.json" 2>> "$OUT/err.log"
     python3 -c "import json; r=json.load(open('$OUT/${tag}_$r.json')); k=r['kernel_ms_per_step']; print('$tag', r['value'], k.get('betti_vr'), k.get('betti_dist'), k.get('graph_emit'))"
   done
