@@ -9,7 +9,12 @@
 //
 // Algorithm (MI355X-first; DESIGN.md "Betti kernel"):
 //   * n <= NP points per complex (NP in {32, 48, 64}): one lane per vertex, 64-bit adjacency
-//     masks, the f32 distance matrix in LDS (stride NP+1, conflict-free row and column reads);
+//     masks, the distance matrix in LDS as u16 RANK CODES (code = index of the distance's first
+//     occurrence among the complex's sorted distances <= thr; 0xFFFF above thr and on the
+//     diagonal): order and equality are all the reduction ever asks of a distance
+//     (ripser.cpp:318-324, 386-395), the f32 values come back from the sorted table only for
+//     the emitted pairs. 2 B per entry keep a 48-point complex in 5 KB of LDS (six waves per
+//     SIMD instead of five with the f32 matrix);
 //   * distance matrix: the K=3 Gram product is built on the matrix cores with
 //     v_mfma_f64_16x16x4_f64 as three rank-1 products (exactly round(x_ik*x_jk) each), summed on
 //     the VALU in the reference's order ((p0+p1)+p2), then sqrt(max(0,(sq_i+sq_j)-2p)) -> f32:
@@ -39,6 +44,7 @@ constexpr int kVStoreCap = 65536; // stored V-list entries per dimension
 constexpr int kNACap = 4096;      // non-apparent columns per dimension (scratch)
 constexpr int kPivCap = 4096;     // serially resolved pivots per dimension
 constexpr int kPairCap = 4096;    // pairs per dimension (scratch)
+constexpr uint32_t kNoCode = 0xFFFFu;  // rank-code matrix: distance above thr, or the diagonal
 #ifndef DGN_CHUNK
 #define DGN_CHUNK 1
 #endif
@@ -94,26 +100,27 @@ struct ScratchLayout {
     // columns whose min-cofacet walk did not finish in the first round of an apparent pass (packed
     // edge or triangle), walked to the end by a second round over this list
     static constexpr int64_t defer = d0 + 4 * 64;                    // uint32 [C(64,3)]
-    static constexpr int64_t total = defer + 4 * (64 * 63 * 62 / 6);
+    // rank codes (rank_codes): the compacted keys of the distances <= thr, and the sorted f32
+    // distances (code -> value, for the emitted pairs)
+    static constexpr int64_t rankk = (defer + 4 * (64 * 63 * 62 / 6) + 15) / 16 * 16;  // uint64 [1024]
+    static constexpr int64_t svals = rankk + 8 * 1024;               // f32 [1024]
+    static constexpr int64_t total = svals + 4 * 1024;
 };
 
-// Per-wave LDS. The tiers are sized for resident waves: NP = 44 (the typical 5 A complex of
-// 43..44 points) fits 8 KB, i.e. 20 waves per CU (5 per SIMD, with __launch_bounds__ capping the
-// VGPRs at 96), where NP = 48 (9.6 KB) keeps 16. The hot reads (rows a, b, c at column k =
-// lane) are conflict-free for any stride; an odd stride also makes column reads conflict-free,
-// kept where it costs no occupancy step.
+// Per-wave LDS: the u16 rank-code matrix, the adjacency masks and the forest. The 48-point tier
+// (every 5 A complex of FCC-256: 43..46 points) takes 5,040 B, so LDS admits 32 waves per CU and
+// the register budget of six waves per SIMD (80 VGPRs, <= 106 SGPRs) binds; the f32 matrix took
+// 8 KB at 44 points (five waves per SIMD) and 9.6 KB at 48 (four). The hot reads (rows a, b, c
+// at column k = lane) are conflict-free (two lanes per bank word).
 template <int NP>
 struct BettiSmem {
-    static constexpr int S = NP == 44 ? NP : NP + 1;
-    float D[NP * S];                  // full symmetric f32 distance matrix, D[i * S + j]
+    static constexpr int S = NP;
+    uint16_t D[NP * S];               // full symmetric rank-code matrix, D[i * S + j]
     uint64_t adj[NP];
     uint8_t par[NP];                  // minimum spanning forest: parent of each vertex (0xFF = root)
 };
-#ifndef DGN_WAVES44
-#define DGN_WAVES44 5
-#endif
 template <int NP>
-constexpr int betti_waves_per_simd() { return NP <= 44 ? DGN_WAVES44 : (NP <= 48 ? 4 : 3); }
+constexpr int betti_waves_per_simd() { return NP <= 48 ? 6 : 4; }
 
 // ---------------------------------------------------------------------------------------
 // small helpers
@@ -141,12 +148,13 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 // F-order key: ascending key == Ripser's filtration order (diameter ascending, then the
-// combinatorial index DESCENDING, greater_diameter_or_smaller_index at ripser.cpp:318-324).
-// Vertex tuples packed 8 bits per vertex in descending order preserve the colex (index) order.
-__device__ __forceinline__ uint64_t make_key(float diam, uint32_t packed) {
-    return ((uint64_t)__float_as_uint(diam) << 32) | (uint64_t)(~packed);
+// combinatorial index DESCENDING, greater_diameter_or_smaller_index at ripser.cpp:318-324), the
+// diameter as its rank code. Vertex tuples packed 8 bits per vertex in descending order preserve
+// the colex (index) order.
+__device__ __forceinline__ uint64_t make_key(uint32_t code, uint32_t packed) {
+    return ((uint64_t)code << 32) | (uint64_t)(~packed);
 }
-__device__ __forceinline__ float key_diam(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+__device__ __forceinline__ uint32_t key_code(uint64_t k) { return (uint32_t)(k >> 32); }
 __device__ __forceinline__ uint32_t key_packed(uint64_t k) { return ~(uint32_t)k; }
 
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return ((uint32_t)a << 8) | (uint32_t)b; }
@@ -219,24 +227,23 @@ struct Complex {
     } while (0)
 #endif
 
-    // Distances are non-negative floats, so their order is the order of their bit patterns:
-    // maxima are taken as unsigned integer maxima (no NaN canonicalization). The matrix is
-    // stored full, so a lookup is one multiply-add whichever vertex is larger.
+    // Distances are rank codes (order- and equality-preserving): maxima are unsigned maxima, and
+    // a simplex through a pair above thr (or a repeated vertex) gets kNoCode by the maximum
+    // alone. The matrix is stored full, so a lookup is one multiply-add whichever vertex is
+    // larger; loads zero-extend the u16 code.
     static constexpr int S = BettiSmem<NP>::S;
-    __device__ const uint32_t* Db() const { return reinterpret_cast<const uint32_t*>(s.D); }
+    uint32_t zero_code;  // code of the distance 0.0f if the complex has one, else ~0u
+    __device__ const uint16_t* Db() const { return s.D; }
     __device__ uint32_t dlowb(int a, int b) const { return Db()[a * S + b]; }
     __device__ uint32_t db(int i, int j) const { return Db()[i * S + j]; }
-    __device__ float dlow(int a, int b) const { return __uint_as_float(dlowb(a, b)); }
-    __device__ float dist(int i, int j) const { return __uint_as_float(db(i, j)); }
     __device__ uint64_t ekey(int i, int j) const {  // i != j; reads row i (Prim: i uniform)
         const int a = max(i, j), b = min(i, j);
-        return make_key(dist(i, j), pack2(a, b));
+        return make_key(db(i, j), pack2(a, b));
     }
     __device__ uint32_t tri_diamb(int a, int b, int c) const {  // a > b > c
         return max(max(dlowb(a, b), dlowb(a, c)), dlowb(b, c));
     }
-    __device__ float tri_diam(int a, int b, int c) const { return __uint_as_float(tri_diamb(a, b, c)); }
-    __device__ uint64_t tkey(int a, int b, int c) const { return make_key(tri_diam(a, b, c), pack3(a, b, c)); }
+    __device__ uint64_t tkey(int a, int b, int c) const { return make_key(tri_diamb(a, b, c), pack3(a, b, c)); }
     // tree edge (i, j): one is the other's parent in the spanning forest
     __device__ bool is_tree(int i, int j) const { return s.par[i] == j || s.par[j] == i; }
     // clearing marks live in the triangle min-cofacet table (scratch) until the dim-2 pass
@@ -252,18 +259,10 @@ struct Complex {
     }
     template <typename T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scratch + off); }
+    // pairs (birth, death): rank codes during the reduction (uint2), decoded in place to f32
+    // (float2) before the statistics (decode_outputs)
     __device__ float2* pairs(int dim) const { return sp<float2>(dim == 1 ? ScratchLayout::p1 : ScratchLayout::p2); }
-
-    // wave-uniform: append pairs (birth, death) for lanes with `emit`
-    __device__ void append_pairs(int dim, bool emit, float birth, float death) {
-        const uint64_t bal = ballot(emit);
-        int& np = dim == 1 ? n_p1 : n_p2;
-        if (emit) {
-            const int slot = np + mask_prefix(bal);
-            if (slot < kPairCap) at(pairs(dim), slot) = make_float2(birth, death);
-        }
-        np += __popcll(bal);
-    }
+    __device__ uint2* pair_codes(int dim) const { return sp<uint2>(dim == 1 ? ScratchLayout::p1 : ScratchLayout::p2); }
 
     // per-lane: F-minimal cofacet key of edge (a > b) / triangle (a > b > c) over cand (kInf if
     // cand is empty). For one simplex, inserting a larger vertex k gives a larger packed tuple,
@@ -281,9 +280,9 @@ struct Complex {
         bk = -1;
         found = false;
         hda = hdb = hdc = 0u;
-        const uint32_t* ra = Db() + a * S;  // rows a, b, c: entry k is d(., k)
-        const uint32_t* rb = Db() + b * S;
-        const uint32_t* rcv = Db() + c * S;
+        const uint16_t* ra = Db() + a * S;  // rows a, b, c: entry k is d(., k)
+        const uint16_t* rb = Db() + b * S;
+        const uint16_t* rcv = Db() + c * S;
         // the candidates bit-reversed: the largest remaining k is the lowest set bit, taken with a
         // trailing-zero count and cleared with r & (r - 1) (no validity select: 0 stays 0)
         uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)cand) << 32) | __builtin_bitreverse32((uint32_t)(cand >> 32));
@@ -402,7 +401,7 @@ struct Complex {
     // entry t + 64 (set 1) with its diameter. Toggles only move packed simplices; pivot_of_V
     // refreshes the diameters lane-parallel and reads entries back uniformly with v_readlane.
     uint32_t vs0 = 0, vs1 = 0;
-    float vd0 = 0.f, vd1 = 0.f;
+    uint32_t vd0 = 0, vd1 = 0;
 
     __device__ static uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
     __device__ static uint64_t rl64(uint64_t x, int l) {
@@ -438,8 +437,8 @@ struct Complex {
         v = (int)uni((uint32_t)(v + 1));
         return true;
     }
-    __device__ float simplex_diam(int dim, uint32_t x) const {
-        return dim == 1 ? dlow((x >> 8) & 255, x & 255) : tri_diam((x >> 16) & 255, (x >> 8) & 255, x & 255);
+    __device__ uint32_t simplex_diam(int dim, uint32_t x) const {
+        return dim == 1 ? dlowb((x >> 8) & 255, x & 255) : tri_diamb((x >> 16) & 255, (x >> 8) & 255, x & 255);
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
@@ -449,8 +448,8 @@ struct Complex {
     // tau in V, always in a different lane (k = tau \ s), so the multiplicity of the wave
     // minimum is the popcount of a ballot. Even multiplicity: raise the floor and repeat.
     // kInf for the zero column.
-    // key of the cofacet s u {k} for lane k (k < n); its high word is 0xFFFFFFFF (above every real
-    // key) if k is not a common neighbour of s: the LDS matrix holds all-ones for distances above
+    // key of the cofacet s u {k} for lane k (k < n); its high word is kNoCode (above every real
+    // key) if k is not a common neighbour of s: the LDS matrix holds kNoCode for distances above
     // thr and on the diagonal, so the diameter maximum carries it. The low word, ~packed(tau), is
     // built in one v_perm_b32 from the complemented tuple of s (nsp = ~sp_) and lane k's
     // complemented vertex byte (kc = 255 - k, perm byte 4), with the byte order picked by where k
@@ -512,8 +511,8 @@ struct Complex {
             };
             // lanes k >= n are not vertices: they keep kInf (exec-masked, no per-entry test)
             if (k < n) {
-                scan(vs0, __float_as_uint(vd0), v < 64 ? v : 64);
-                if (v > 64) scan(vs1, __float_as_uint(vd1), v - 64);
+                scan(vs0, vd0, v < 64 ? v : 64);
+                if (v > 64) scan(vs1, vd1, v - 64);
             }
             // wave minimum: the high words first; a unique minimal high word settles it (and its
             // multiplicity, 1) without the low-word stage
@@ -534,9 +533,9 @@ struct Complex {
 #ifdef DGN_PHASE_TIMING
             if (tagged()) { ph[24] += 1; ph[25] += (uint64_t)v; }
 #endif
-            // no cofacet above floor: the minimum is a non-neighbour key (high word all ones) or
-            // a wrapped key <= floor
-            if ((uint32_t)(m >> 32) == 0xFFFFFFFFu || m <= floor) return kInf;
+            // no cofacet above floor: the minimum is a non-neighbour key (high word kNoCode; every
+            // lane without a cofacet: all ones) or a wrapped key <= floor
+            if ((uint32_t)(m >> 32) >= kNoCode || m <= floor) return kInf;
             if (mult & 1) return m;
             floor = m;
         }
@@ -548,6 +547,23 @@ struct Complex {
         const uint32_t f = max_facet(dim, tau);
         const uint32_t m = at(mincof_of(dim), col_dense(dim, f));
         return m == extra_vertex(key_packed(tau), f) ? f : kNone;
+    }
+
+    // dim-0 deaths and the dim-1 / dim-2 pairs: rank codes -> f32 (the complex's decode table),
+    // in place (each lane rewrites its own entries)
+    __device__ void decode_outputs(uint32_t* d0s) const {
+        const int lane = lane_id();
+        const float* sv = sp<float>(ScratchLayout::svals);
+        __syncthreads();  // the decode table and the code lists (scratch) were written by other lanes
+        for (int i = lane; i < n_d0; i += kWave) at(d0s, i) = __float_as_uint(at(sv, at(d0s, i)));
+        for (int d = 1; d <= 2; ++d) {
+            const int np = min(d == 1 ? n_p1 : n_p2, kPairCap);
+            for (int i = lane; i < np; i += kWave) {
+                const uint2 c = at(pair_codes(d), i);
+                at(pairs(d), i) = make_float2(at(sv, c.x), at(sv, c.y));
+            }
+        }
+        __syncthreads();
     }
 
     // Walk the non-apparent columns in Ripser's order (whole wave). na_* (scratch) hold each
@@ -631,7 +647,7 @@ struct Complex {
             colkey = uni64(colkey);
             tau = uni64(tau);
             const uint32_t cp = key_packed(colkey);
-            const float birth = key_diam(colkey);
+            const uint32_t birth = key_code(colkey);
             DGN_SUB(17);
             int owner = (int)uni((uint32_t)find_pivot(npiv, tau));
             DGN_SUB(18);
@@ -699,11 +715,11 @@ struct Complex {
                 if (tau == kInf) continue;  // zero column
             }
             // ---- tau is the pivot of this column ----
-            const float death = key_diam(tau);
-            if (death > birth) {
+            const uint32_t death = key_code(tau);
+            if (death > birth) {  // codes order as the distances (ripser.cpp:1240)
                 if (lane == 0) {
                     const int slot = dim == 1 ? n_p1 : n_p2;
-                    if (slot < kPairCap) at(pairs(dim), slot) = make_float2(birth, death);
+                    if (slot < kPairCap) at(pair_codes(dim), slot) = make_uint2(birth, death);
                 }
                 if (dim == 1) ++n_p1;
                 else ++n_p2;
@@ -753,6 +769,176 @@ struct Complex {
 #define DGN_STOP(k)
 #endif
 
+// Ascending bitonic sort of 64 R keys in registers, element e = lane * R + r: exchanges at a
+// distance j < R stay in the lane (registers r and r ^ j), the others pair lane with lane ^ (j / R)
+// (ds_bpermute). Merge levels k < R are unrolled (directions known per register); from k = R on
+// the direction is a lane bit and the levels run as a loop (a short kernel: the sort runs once
+// per complex next to the reduction's hot loops in the instruction cache).
+template <int R>
+__device__ __forceinline__ void bitonic_in_lane(uint64_t (&x)[R], int j, bool asc) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r & j) continue;
+        const uint64_t a = x[r], b = x[r | j];
+        const bool sw = (a > b) == asc;
+        x[r] = sw ? b : a;
+        x[r | j] = sw ? a : b;
+    }
+}
+template <int R>
+__device__ __forceinline__ void bitonic_sort_regs(uint64_t (&x)[R], int lane) {
+    constexpr int P = kWave * R;
+#pragma unroll
+    for (int k = 2; k < R; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (r & j) continue;
+                const bool asc = (r & k) == 0;
+                const uint64_t a = x[r], b = x[r | j];
+                const bool sw = (a > b) == asc;
+                x[r] = sw ? b : a;
+                x[r | j] = sw ? a : b;
+            }
+        }
+    }
+#pragma unroll 1
+    for (int k = R; k <= P; k <<= 1) {
+        const bool asc = k >= P || (lane & (k / R)) == 0;  // bit k of e
+#pragma unroll 1
+        for (int j = k >> 1; j >= R; j >>= 1) {
+            const int lm = j / R;
+            const bool keep_min = ((lane & lm) == 0) == asc;
+            // four registers' exchanges in flight together
+#pragma unroll
+            for (int r0 = 0; r0 < R; r0 += 4) {
+                uint64_t p[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) p[q] = shfl_xor64(x[r0 + q], lm);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x[r0 + q] = ((p[q] < x[r0 + q]) == keep_min) ? p[q] : x[r0 + q];
+            }
+        }
+#pragma unroll
+        for (int j = R >> 1; j > 0; j >>= 1) bitonic_in_lane<R>(x, j, asc);
+    }
+}
+
+// Rank codes of one complex (one wave): the packed f32 lower triangle (ripser_wrapper.cpp:20-24
+// packing) becomes the full u16 matrix s.D of codes -- code(d) = the index of d's first
+// occurrence among the complex's sorted distances <= thr (order- and equality-preserving),
+// kNoCode above thr (sparse_distance_matrix keeps d <= thr, ripser.cpp:386-395) and on the
+// diagonal -- and sv_out[code] = d (the decode table). The m distances <= thr are compacted
+// (ballots) into scratch as (f32 bits << 12 | i << 6 | j) keys, sorted in registers (bitonic, R
+// per lane: 512 or 1,024 keys), and each sorted key scatters its run's first index to (i, j) and
+// (j, i). Returns the code of 0.0f if the complex has a zero distance, ~0u if it has none, and
+// kRankDense if more than kRankMax<NP> distances are <= thr (R = 8 registers per lane in the
+// 32- and 48-point tiers: 512 keys, the dense launch takes the rest; 16 in the 64-point tier:
+// 1,024, the capacity retry takes the rest).
+constexpr uint32_t kRankDense = 0xFFFFFFFEu;
+template <int NP>
+constexpr int kRankMax = NP <= 48 ? 512 : 1024;
+template <int R>
+__device__ __forceinline__ uint32_t rank_sorted(uint16_t* D, int S, const uint64_t* keys, int m, float* sv_out,
+                                                int lane) {
+    uint64_t x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane * R + r;
+        x[r] = e < m ? at(keys, e) : ~0ull;
+    }
+    bitonic_sort_regs<R>(x, lane);
+    // code = the first index of the element's value run = the running maximum of (e if element
+    // e starts a run, else 0): within the lane, then across lanes (exclusive max-scan)
+    const uint32_t prev_bits = (uint32_t)__shfl_up((int)(uint32_t)(x[R - 1] >> 12), 1, kWave);
+    uint32_t c[R];
+    uint32_t run = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t bits = (uint32_t)(x[r] >> 12);
+        const bool first = r == 0 ? (lane == 0 || bits != prev_bits) : bits != (uint32_t)(x[r - 1] >> 12);
+        run = first ? (uint32_t)(lane * R + r) : run;
+        c[r] = run;
+    }
+    uint32_t carry = c[R - 1];
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t w = (uint32_t)__shfl_up((int)carry, o, kWave);
+        carry = lane >= o ? max(carry, w) : carry;
+    }
+    uint32_t in = (uint32_t)__shfl_up((int)carry, 1, kWave);
+    in = lane == 0 ? 0u : in;
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = max(c[r], in);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int e = lane * R + r;
+        if (e < m) {
+            const uint32_t k = (uint32_t)x[r];
+            const int i = (k >> 6) & 63, j = k & 63;
+            D[i * S + j] = (uint16_t)c[r];
+            D[j * S + i] = (uint16_t)c[r];
+            at(sv_out, e) = __uint_as_float((uint32_t)(x[r] >> 12));
+        }
+    }
+    (void)S;
+    return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x[0] >> 12), 0)) == 0.0f && m > 0
+               ? 0u
+               : 0xFFFFFFFFu;
+}
+
+template <int NP>
+__device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __restrict__ L, int n, float thr,
+                                               float* sv_out, uint64_t* keys) {
+    constexpr int S = BettiSmem<NP>::S;
+    const int lane = lane_id();
+    const int tot = c2(n);
+    // the matrix starts as kNoCode everywhere (pairs above thr, the diagonal)
+    {
+        uint32_t* Dw = reinterpret_cast<uint32_t*>(s.D);
+        for (int w = lane; w < NP * S / 2; w += kWave) Dw[w] = (kNoCode << 16) | kNoCode;
+    }
+    // (1) compaction of the distances <= thr into scratch keys, t-order; lane l holds entries
+    // t = l + 64 u, its (i, j) advanced incrementally (entry t of the packing is row i, column
+    // t - c2(i))
+    int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)lane)) * 0.5f);
+    i -= c2(i) > lane;
+    i += c2(i + 1) <= lane;
+    int j = lane - c2(i);
+    int m = 0;
+    for (int t0 = 0; t0 < tot; t0 += 2 * kWave) {
+        const int t = t0 + lane;
+        const float v0 = t < tot ? at(L, t) : INFINITY;
+        const float v1 = t + kWave < tot ? at(L, t + kWave) : INFINITY;
+        const int i0 = i, j0 = j;
+        j += kWave;
+        while (j >= i) { j -= i; ++i; }
+        const int i1 = i, j1 = j;
+        j += kWave;
+        while (j >= i) { j -= i; ++i; }
+        const bool ok0 = v0 <= thr, ok1 = v1 <= thr;
+        const uint64_t b0 = ballot(ok0), b1 = ballot(ok1);
+        if (ok0 && m + mask_prefix(b0) < 1024)
+            at(keys, m + mask_prefix(b0)) = ((uint64_t)__float_as_uint(v0) << 12) | (uint64_t)((i0 << 6) | j0);
+        m += __popcll(b0);
+        if (ok1 && m + mask_prefix(b1) < 1024)
+            at(keys, m + mask_prefix(b1)) = ((uint64_t)__float_as_uint(v1) << 12) | (uint64_t)((i1 << 6) | j1);
+        m += __popcll(b1);
+    }
+    m = (int)uni((uint32_t)m);
+    if (m > kRankMax<NP>) return kRankDense;
+    __syncthreads();  // the keys (scratch) are read by other lanes
+    uint32_t z;
+    if constexpr (NP <= 48) {
+        z = rank_sorted<8>(s.D, S, keys, m, sv_out, lane);
+    } else {
+        z = m <= 512 ? rank_sorted<8>(s.D, S, keys, m, sv_out, lane) : rank_sorted<16>(s.D, S, keys, m, sv_out, lane);
+    }
+    lds_sync();
+    return z;
+}
+
 template <int NP>
 __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
@@ -770,8 +956,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
         lane = lane_id();
         asm volatile("" : "+v"(lane));
     };
-    // all-ones diagonal (never overwritten): no vertex is its own common neighbour (cofacet_key)
-    if (lane < NP) s.D[lane * BettiSmem<NP>::S + lane] = __uint_as_float(0xFFFFFFFFu);
     uint8_t* scratch = bl.scratch + (int64_t)blockIdx.x * bl.scratch_per_wave;
     const int64_t A = bl.num_atoms;
 
@@ -811,43 +995,30 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             uint8_t* cscr = scratch;
             asm volatile("" : "+s"(cscr));
             Complex<NP> cx{s, n, bl.thr, cscr, 0u, 0, 0, 0, 0, 0, 0};
+            cx.zero_code = 0xFFFFFFFFu;
 #ifdef DGN_PHASE_TIMING
             cx.ph = ph;
             cx.tprev = &t_prev;
 #endif
             DGN_PHASE(7);
             constexpr int S = BettiSmem<NP>::S;
-            {
-                // f32 strict lower triangle (ripser_wrapper.cpp:20-24 packing), mirrored into
-                // the full matrix; one coalesced read per row
-                // entry t of the packing is (i, j) with i = floor((1 + sqrt(1 + 8t)) / 2), j = t - c2(i);
-                // all loads of a lane are independent, four in flight per step
-                const float* L = bl.lower + gi * bl.tri_stride;
-                const int tot = c2(n);
-                for (int t0 = 0; t0 < tot; t0 += 4 * kWave) {
-                    float v[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = t0 + u * kWave + lane;
-                        v[u] = t < tot ? at(L, t) : 0.0f;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int t = t0 + u * kWave + lane;
-                        int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
-                        i -= c2(i) > t;
-                        i += c2(i + 1) <= t;
-                        const int j = t - c2(i);
-                        // distances above thr are never read as lengths (every simplex of the
-                        // complex has edges <= thr): stored as all-ones, so a cofacet through a
-                        // non-neighbour gets an all-ones diameter by the maximum alone
-                        const float w = v[u] <= cx.thr ? v[u] : __uint_as_float(0xFFFFFFFFu);
-                        if (t < tot) {
-                            s.D[i * S + j] = w;
-                            s.D[j * S + i] = w;
-                        }
-                    }
+            cx.zero_code = rank_codes<NP>(s, bl.lower + gi * bl.tri_stride, n, cx.thr,
+                                          cx.template sp<float>(ScratchLayout::svals),
+                                          cx.template sp<uint64_t>(ScratchLayout::rankk));
+            if (cx.zero_code == kRankDense) {
+                // more distances <= thr than this tier's register sort holds: the dense launch
+                // (NP = 64, 1,024 keys) after this one, or beyond that the capacity-retry launch
+                // (wide kernel, f32 matrix), reduces the complex and writes its outputs
+                if (NP <= 48 && bl.dense_list) {
+                    if (lane == 0) bl.dense_list[atomicAdd(bl.dense_len, 1u)] = (int32_t)gi;
+                } else if (bl.retry_list) {
+                    if (lane == 0) bl.retry_list[atomicAdd(bl.retry_len, 1u)] = (int32_t)gi;
+                } else {
+                    if (lane == 0) atomicOr(bl.error_flag, kErrWorkCol);
+                    if (feat && lane < 35) feat[lane] = __builtin_nan("");
+                    if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
                 }
+                continue;
             }
             lds_sync();
             DGN_PHASE(0); DGN_STOP(1)
@@ -856,13 +1027,13 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             uint64_t myadj = 0;  // this lane's row
             {
                 for (int i = 0; i < n; ++i) {
-                    // the all-ones diagonal (NaN) fails the test: no self loops
-                    const uint64_t row = ballot(s.D[i * S + lane] <= cx.thr) & lanes_below(n);
+                    // the kNoCode diagonal fails the test: no self loops
+                    const uint64_t row = ballot(s.D[i * S + lane] != kNoCode) & lanes_below(n);
                     myadj = lane == i ? row : myadj;
                 }
                 if (lane < NP) s.adj[lane] = myadj;  // (lanes >= NP would write past adj)
             }
-            float* d0s = cx.template sp<float>(ScratchLayout::d0);
+            uint32_t* d0s = cx.template sp<uint32_t>(ScratchLayout::d0);  // codes; f32 after decode_outputs
             const int dim_max = n - 2 < 2 ? n - 2 : 2;  // ripser.cpp:560
             cx.n_inf0 = 0;
             cx.n_d0 = 0;
@@ -875,7 +1046,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             {
                 bool in_tree = lane == 0, root = lane == 0;
                 int parent = 0;
-                float death = 0.f;
+                uint32_t death = 0;  // rank code
                 uint64_t best = kInf;
                 if (lane < n && lane != 0 && (myadj & 1ull)) best = cx.ekey(0, lane);
                 if (n >= 1) cx.n_inf0 = 1;
@@ -896,8 +1067,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                             bal = ballot(best == (((uint64_t)mh << 32) | ml));
                         }
                         v = __ffsll((unsigned long long)bal) - 1;
-                        if (__uint_as_float(mh) != 0.0f) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
-                            death = lane == cx.n_d0 ? __uint_as_float(mh) : death;
+                        if (mh != cx.zero_code) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
+                            death = lane == cx.n_d0 ? mh : death;
                             cx.n_d0 += 1;
                         }
                     }
@@ -958,11 +1129,10 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         const int i = ed >> 8, j = ed & 255;
                         uint32_t mc = kMcNone;
                         if (!cx.is_tree(i, j)) {
-                            const float birth = cx.dlow(i, j);
-                            colkey = make_key(birth, pack2(i, j));
+                            const uint32_t dij = cx.dlowb(i, j);
+                            colkey = make_key(dij, pack2(i, j));
                             uint64_t cand = s.adj[i] & s.adj[j];
                             if (cand) {
-                                const uint32_t dij = __float_as_uint(birth);
                                 int bk;
                                 bool found;
                                 uint32_t hda, hdb, hdc;
@@ -1099,7 +1269,7 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         if (clb != kMcCleared) {
                             const uint32_t dab = cx.dlowb(a, b), dac = cx.dlowb(a, c), dbc = cx.dlowb(b, c);
                             const uint32_t ds = max(max(dab, dac), dbc);
-                            colkey = make_key(__uint_as_float(ds), tp);
+                            colkey = make_key(ds, tp);
                             uint64_t cand = s.adj[a] & s.adj[b] & s.adj[c];
                             if (cand) {
                                 int bk;
@@ -1199,11 +1369,13 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             } else {
                 // ---- statistics (betti_features.cpp:24-55, 87-98; utils/math.hpp:9-28) ----
                 relane();
-                const double myval = betti_stats35(d0s, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
+                cx.decode_outputs(d0s);
+                const float* d0f = reinterpret_cast<const float*>(d0s);
+                const double myval = betti_stats35(d0f, cx.n_d0, cx.pairs(1), cx.n_p1, cx.pairs(2), cx.n_p2, weight);
                 if (feat && lane < 35) at(feat, lane) = myval;
                 if (bl.pairs_out) {
                     float2* po = reinterpret_cast<float2*>(bl.pairs_out) + (int64_t)gi * 3 * bl.pair_cap;
-                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) at(po, i) = make_float2(0.0f, at(d0s, i));
+                    for (int i = lane; i < cx.n_d0 && i < bl.pair_cap; i += kWave) at(po, i) = make_float2(0.0f, at(d0f, i));
                     for (int i = lane; i < cx.n_p1 && i < bl.pair_cap; i += kWave) at(po, bl.pair_cap + i) = at(cx.pairs(1), i);
                     for (int i = lane; i < cx.n_p2 && i < bl.pair_cap; i += kWave) at(po, 2 * bl.pair_cap + i) = at(cx.pairs(2), i);
                 }
@@ -1273,9 +1445,7 @@ hipError_t betti_init_scratch(hipStream_t s, uint8_t* base, int slots) {
     return hipMemset2DAsync(base + ScratchLayout::mincof, (size_t)ScratchLayout::total, kMcNone, width, (size_t)slots, s);
 }
 
-static int np_for(int max_points) {
-    return max_points <= 32 ? 32 : (max_points <= 44 ? 44 : (max_points <= 48 ? 48 : 64));
-}
+static int np_for(int max_points) { return max_points <= 32 ? 32 : (max_points <= 48 ? 48 : 64); }
 
 int betti_grid_waves(int device) {
     hipDeviceProp_t prop;
@@ -1287,9 +1457,8 @@ int betti_grid_waves(int device) {
     return prop.multiProcessorCount * per_cu;
 }
 
-// route complexes above np_small points: up to np_mid to the mid list (NP = 48 launch), up to
-// 64 to the overflow list (NP = 64 launch), above 64 to the wide list (betti_wide_kernel);
-// wave-aggregated appends
+// route complexes above np_small points: up to 64 to the overflow list (NP = 64 launch), above 64
+// to the wide list (betti_wide_kernel), above kWideRegular to the retry list; wave-aggregated appends
 __device__ __forceinline__ void bucket_append(bool take, int32_t* list, uint32_t* len, int64_t gi) {
     const uint64_t b = ballot(take);
     if (!b) return;
@@ -1299,16 +1468,14 @@ __device__ __forceinline__ void bucket_append(bool take, int32_t* list, uint32_t
     base = (uint32_t)__shfl((int)base, leader, kWave);
     if (take) list[base + mask_prefix(b)] = (int32_t)gi;
 }
-__global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small, int np_mid) {
+__global__ __launch_bounds__(256) void betti_bucket_kernel(BettiLaunch bl, int np_small) {
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int n = gi < bl.num_atoms ? bl.npoints[gi] : 0;
-    const bool tier48 = gi < bl.num_atoms && n > np_small && n <= np_mid;
-    const bool mid = gi < bl.num_atoms && n > np_mid && n <= 64;
+    const bool mid = gi < bl.num_atoms && n > np_small && n <= 64;
     // above kWideRegular points: straight to the retry list (rank-coded BIG launch)
     const bool huge = gi < bl.num_atoms && n > kWideRegular && bl.retry_list;
     const bool wide = gi < bl.num_atoms && n > 64 && !huge;
     bucket_append(huge, bl.retry_list, bl.retry_len, gi);
-    bucket_append(tier48, bl.mid_list, bl.mid_len, gi);
     bucket_append(mid, bl.overflow_list, bl.overflow_len, gi);
     bucket_append(wide, bl.wide_list, bl.wide_len, gi);
 }
@@ -1329,6 +1496,9 @@ static int cu_count(int dev) {
     return v;
 }
 
+#ifndef DGN_PAD_LDS
+#define DGN_PAD_LDS 0  // A/B builds only: extra dynamic LDS per wave (lower residency)
+#endif
 template <int NP>
 static int grid_np(int grid_waves, int64_t max_items) {
     int dev = 0, per_cu = 0;
@@ -1337,7 +1507,7 @@ static int grid_np(int grid_waves, int64_t max_items) {
     if (dev >= 0 && dev < 64 && occ[dev].load(std::memory_order_relaxed) > 0) {
         per_cu = occ[dev].load(std::memory_order_relaxed);
     } else {
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, betti_kernel<NP>, kWave, DGN_PAD_LDS);
         if (e != hipSuccess || per_cu <= 0) per_cu = 4;
         if (dev >= 0 && dev < 64) occ[dev].store(per_cu, std::memory_order_relaxed);
     }
@@ -1350,41 +1520,38 @@ static int grid_np(int grid_waves, int64_t max_items) {
 
 static int grid_for(int np, int grid_waves, int64_t max_items) {
     if (np == 32) return grid_np<32>(grid_waves, max_items);
-    if (np == 44) return grid_np<44>(grid_waves, max_items);
     if (np == 48) return grid_np<48>(grid_waves, max_items);
     return grid_np<64>(grid_waves, max_items);
 }
 
 template <int NP>
 static hipError_t launch_np(hipStream_t st, const BettiLaunch& b, int grid) {
-    hipLaunchKernelGGL(betti_kernel<NP>, dim3(grid), dim3(kWave), 0, st, b);
+    hipLaunchKernelGGL(betti_kernel<NP>, dim3(grid), dim3(kWave), DGN_PAD_LDS, st, b);
     return hipGetLastError();
 }
 
 static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int grid) {
     if (np == 32) return launch_np<32>(st, b, grid);
-    if (np == 44) return launch_np<44>(st, b, grid);
     if (np == 48) return launch_np<48>(st, b, grid);
     return launch_np<64>(st, b, grid);
 }
 
-// Tiered dispatch: the main launch uses the instantiation sized for typical complexes (NP = 44:
-// 20 resident waves per CU); complexes above it are listed by betti_bucket_kernel and reduced by
-// an NP = 48 launch (45..48 points, 16 waves per CU) after the main one, an NP = 64 launch
-// (49..64 points) forked beside it, and betti_wide_kernel (65..512 points). Counters and list
-// lengths live on the device, so nothing synchronizes with the host in between.
+// Tiered dispatch: the main launch uses the instantiation sized for typical complexes (NP = 48:
+// 24 resident waves per CU); complexes above it are listed by betti_bucket_kernel and reduced by
+// an NP = 64 launch (49..64 points) forked beside the main one and betti_wide_kernel (65..512
+// points). Counters and list lengths live on the device, so nothing synchronizes with the host in
+// between.
 hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, int grid_waves, const WideLayout* wide,
                         int wide_waves, const BettiFork* fork) {
     const int np_big = np_for(max_points < 64 ? max_points : 64);
-    const int np_main = np_big > 44 ? 44 : np_big;
-    const int np_mid = np_big > 44 ? 48 : np_main;  // tier 48 only when the main tier is 44
+    const int np_main = np_big > 48 ? 48 : np_big;
     BettiLaunch m = b;
     m.work_list = nullptr;
     m.queue = b.work_counter;
     m.skip_above = max_points > np_main ? 1 : 0;
     if (m.skip_above) {
         const int64_t blocks = (b.num_atoms + 255) / 256;
-        hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main, np_mid);
+        hipLaunchKernelGGL(betti_bucket_kernel, dim3((unsigned)blocks), dim3(256), 0, st, b, np_main);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -1409,15 +1576,19 @@ hipError_t launch_betti(hipStream_t st, const BettiLaunch& b, int max_points, in
         if ((e = hipEventRecord(fork->join, fork->side)) != hipSuccess) return e;
     }
     e = launch_for(np_main, st, m, main_grid);
-    if (e != hipSuccess || !m.skip_above) return e;
-    if (np_mid > np_main) {
-        BettiLaunch t = b;
-        t.work_list = b.mid_list;
-        t.work_len = b.mid_len;
-        t.queue = b.work_counter3;
-        t.skip_above = 0;
-        if ((e = launch_for(48, st, t, grid_for(48, main_grid, b.num_atoms))) != hipSuccess) return e;
+    if (e != hipSuccess) return e;
+    {
+        // complexes the main launch listed as dense (more than 512 distances <= thr): NP = 64
+        // launch on the main grid's scratch slots; its waves leave at once when the list is empty
+        BettiLaunch d = b;
+        d.work_list = b.dense_list;
+        d.work_len = b.dense_len;
+        d.queue = b.dense_queue;
+        d.skip_above = 0;
+        d.dense_list = nullptr;
+        if ((e = launch_for(64, st, d, grid_for(64, main_grid, b.num_atoms))) != hipSuccess) return e;
     }
+    if (!m.skip_above) return e;
     if (overflow) {
         if (fork) {
             if ((e = hipStreamWaitEvent(st, fork->join, 0)) != hipSuccess) return e;

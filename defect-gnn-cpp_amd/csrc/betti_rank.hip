@@ -23,8 +23,14 @@ __global__ __launch_bounds__(kRankBlock) void rank_gather_kernel(const float* __
                                                                  const int32_t* __restrict__ list, int64_t count,
                                                                  int64_t stride, uint32_t* __restrict__ keys,
                                                                  uint32_t* __restrict__ vals, int32_t* __restrict__ beg,
-                                                                 int32_t* __restrict__ end) {
+                                                                 int32_t* __restrict__ end,
+                                                                 const uint32_t* __restrict__ dev_len) {
     const int64_t r = blockIdx.y;
+    // slots past the list's length on the device (launches sized by an upper bound): empty segments
+    if (dev_len && r >= (int64_t)*dev_len) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) beg[r] = end[r] = (int32_t)(r * stride);
+        return;
+    }
     const int64_t gi = list[r];
     const int64_t n = npoints[gi];
     const int64_t m = n * (n - 1) / 2;
@@ -43,8 +49,10 @@ __global__ __launch_bounds__(kRankBlock) void rank_codes_kernel(const int32_t* _
                                                                 const int32_t* __restrict__ list, int64_t stride,
                                                                 const uint32_t* __restrict__ sorted,
                                                                 const uint32_t* __restrict__ pos,
-                                                                uint32_t* __restrict__ codes) {
+                                                                uint32_t* __restrict__ codes,
+                                                                const uint32_t* __restrict__ dev_len) {
     const int64_t r = blockIdx.y;
+    if (dev_len && r >= (int64_t)*dev_len) return;
     const int64_t n = npoints[list[r]];
     const int64_t m = n * (n - 1) / 2;
     const uint32_t* S = sorted + r * stride;
@@ -101,7 +109,7 @@ size_t betti_rank_temp_bytes(int64_t count, int64_t stride) {
 
 hipError_t betti_rank_codes(hipStream_t s, const float* lower, int64_t tri_stride, const int32_t* npoints,
                             const int32_t* list, int64_t count, int64_t stride, uint32_t* codes, uint32_t* sorted,
-                            void* temp, size_t temp_bytes) {
+                            void* temp, size_t temp_bytes, const uint32_t* dev_len) {
     if (count <= 0) return hipSuccess;
     if (count * stride > INT32_MAX) return hipErrorInvalidValue;  // rocprim item counts are 32-bit
     size_t sb = sort_temp_bytes(count, stride);
@@ -110,14 +118,35 @@ hipError_t betti_rank_codes(hipStream_t s, const float* lower, int64_t tri_strid
     const int64_t per = (stride + kRankBlock - 1) / kRankBlock;
     const dim3 grid((unsigned)(per < 64 ? per : 64), (unsigned)count);
     hipLaunchKernelGGL(rank_gather_kernel, grid, dim3(kRankBlock), 0, s, lower, tri_stride, npoints, list, count,
-                       stride, t.keys, t.vals, t.beg, t.end);
+                       stride, t.keys, t.vals, t.beg, t.end, dev_len);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = rocprim::segmented_radix_sort_pairs(t.sort_tmp, sb, (const uint32_t*)t.keys, sorted, (const uint32_t*)t.vals,
                                             t.pos, (unsigned int)(count * stride), (unsigned int)count,
                                             (const int32_t*)t.beg, (const int32_t*)t.end, 0, 32, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rank_codes_kernel, grid, dim3(kRankBlock), 0, s, npoints, list, stride, sorted, t.pos, codes);
+    hipLaunchKernelGGL(rank_codes_kernel, grid, dim3(kRankBlock), 0, s, npoints, list, stride, sorted, t.pos, codes,
+                       dev_len);
+    return hipGetLastError();
+}
+
+// slice q of a list of *total entries: sl[2q] = its length, clamp(*total - q slice, 0, slice), and
+// sl[2q + 1] = 0 (its launch's work queue), for q < nsl -- so the slices of a list whose length
+// only the device knows are launched without a host read (grids sized by the host's upper bound)
+__global__ void slice_lengths_kernel(const uint32_t* __restrict__ total, int64_t slice, int64_t nsl,
+                                     uint32_t* __restrict__ sl) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nsl; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t left = (int64_t)*total - q * slice;
+        sl[2 * q] = (uint32_t)(left < 0 ? 0 : (left < slice ? left : slice));
+        sl[2 * q + 1] = 0u;
+    }
+}
+
+hipError_t launch_slice_lengths(hipStream_t s, const uint32_t* total, int64_t slice, int64_t nsl, uint32_t* sl) {
+    if (nsl <= 0) return hipSuccess;
+    const int64_t blocks = (nsl + 255) / 256;
+    hipLaunchKernelGGL(slice_lengths_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, s, total,
+                       slice, nsl, sl);
     return hipGetLastError();
 }
 

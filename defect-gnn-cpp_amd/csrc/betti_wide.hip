@@ -1314,7 +1314,8 @@ size_t wide_lds_bytes(int nmax) {  // per workgroup: token, adjacency, parents
 // pivot and pair tables of 2^(base_log2 + 2 grow) entries (base_log2 = 24 but for tests), never
 // more than every simplex of the complex needs (C(nmax, 3) columns), and a V store of as many
 // entries. The host raises `grow` while complexes still overflow (kWideMaxGrow levels): a complex
-// outgrows the last level only when its tables exceed 2^(base_log2 + 6) entries.
+// outgrows the last level only when it needs more than kWideMaxCols (2^29) columns, pivots or pairs
+// or a V store above 2^(base_log2 + 6) entries.
 WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, int base_log2) {
     WideLayout l{};
     const int64_t n = nmax;
@@ -1322,6 +1323,9 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
     const bool huge = nmax > kWideBigPoints;
     const int64_t pt = huge ? 8 : 4;  // bytes of a packed column simplex (HUGE: 33-bit triangles)
     int64_t cap_max = big ? (int64_t(1) << (base_log2 + 2 * grow)) : (int64_t(1) << 17);
+    // the pivot hash holds 2 cap entries and is probed with 32-bit masks: columns stop at 2^29
+    // (hash 2^30) so every int32 cap below stays a positive power of two at the last level
+    cap_max = std::min<int64_t>(cap_max, kWideMaxCols);
     if (!big && cap_limit > 0) {
         cap_max = 64;
         while (cap_max < cap_limit) cap_max <<= 1;

@@ -65,6 +65,7 @@ struct Scalars {  // device-side scalars, one allocation
     int64_t total;
     unsigned long long sum_sq;  // sum over atoms of (candidates + 1)^2
     unsigned long long sum_m;   // sum over atoms of candidates (every neighbour within rc)
+    unsigned long long wide_atoms;  // atoms with 64 < candidates + 1 <= kWideRegular (low), above (high)
     uint32_t max_candidates;
     uint32_t max_natoms;        // largest structure of the batch (prep)
     uint32_t graph_flag;        // graph error bits kGErr* (prep, emit, Betti search)
@@ -76,8 +77,9 @@ struct Scalars {  // device-side scalars, one allocation
     uint32_t wide_len;          // complexes routed to the wide launch
     uint32_t retry_len;         // complexes routed to the capacity-retry launch
     uint32_t retry_queue;       // capacity-retry launch queue
-    uint32_t mid_len;           // complexes routed to the mid (NP = 48) launch
-    uint32_t work_counter3;     // betti mid launch queue
+    uint32_t dense_len;         // complexes routed to the dense (NP = 64) launch by the main one
+    uint32_t dense_queue;       // betti dense launch queue
+    uint32_t retry2_len;        // second-level list of the device-driven retry launch (host entry points)
 };
 
 // one neighbour pass's device workspace and the facts its count recorded (count -> emit handshake)
@@ -95,6 +97,7 @@ struct GraphWork {
     int64_t edges = 0;
     double sum_sq = 0;
     double sum_m = 0;  // neighbours within rc over the batch (the K = inf edge count)
+    int64_t wide_atoms = 0, huge_atoms = 0;  // local complexes of 65..kWideRegular / more points
 };
 
 // host-pinned mirror: the scalars after a count pass, and the emit's deferred error flag
@@ -128,6 +131,7 @@ struct dgn_ctx {
     bool betti_pending = false;   // a Betti pass's flags are on their way to host->betti_flags
     DevBuf bflags;                // [kBFWords] sticky Betti words (above)
     int big_nmax = 0, big_waves = 0;  // capacity-retry workspace (b_big) the tables were initialised for
+    int64_t big_budget = 0;           // bytes the device-driven retry workspace may take (first use)
     // betti workspace
     DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_rlist2, b_big, b_rank, b_rscal, b_rank16,
         b_rscal16;
@@ -314,7 +318,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     HIP_TRY(c, W.meta.ensure(sizeof(StructMeta) * (size_t)std::max<int64_t>(B, 1)));
     HIP_TRY(c, W.counts.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.block_sums.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
-    HIP_TRY(c, W.block_aux.ensure(4 * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
+    HIP_TRY(c, W.block_aux.ensure(kAux * sizeof(uint64_t) * (size_t)std::max<int64_t>(nblocks, 1)));
     HIP_TRY(c, W.defer.ensure((size_t)std::max<int64_t>(nblocks, 1)));  // a flag byte per count tile
     HIP_TRY(c, W.atom_struct.ensure(sizeof(int32_t) * A1));
     HIP_TRY(c, W.cell_start.ensure(sizeof(int32_t) * (size_t)(A + B + 1)));
@@ -348,7 +352,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     {
         TimedLaunch t(c, betti ? "betti_nl_scan" : "block_scan", (double)nblocks * 32, 0);
         HIP_TRY(c, launch_block_scan(c->stream, W.block_sums.as<int64_t>(), W.block_aux.as<uint64_t>(), nblocks,
-                                     &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms, &sc->sum_m));
+                                     &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms, &sc->sum_m, &sc->wide_atoms));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->s, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -368,6 +372,8 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
     W.edges = c->host->s.total;
     W.sum_sq = (double)c->host->s.sum_sq;
     W.sum_m = (double)c->host->s.sum_m;
+    W.wide_atoms = (int64_t)(c->host->s.wide_atoms & 0xFFFFFFFFull);
+    W.huge_atoms = (int64_t)(c->host->s.wide_atoms >> 32);
     W.has_weight = want_weight;
     W.species = b->species;
     if (num_edges) *num_edges = W.edges;
@@ -474,7 +480,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         HIP_TRY(c, hipMemsetAsync(c->bflags.p, 0, kBFWords * sizeof(uint32_t), c->stream));
     }
     uint32_t* bflags = c->bflags.as<uint32_t>();
-    HIP_TRY(c, c->b_list.ensure(2 * sizeof(int32_t) * (size_t)A));  // overflow list, mid list
+    HIP_TRY(c, c->b_list.ensure(2 * sizeof(int32_t) * (size_t)A));  // overflow list, dense list
     // complexes above 64 points: the wide kernel, one wave per complex with a per-wave scratch
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
     WideLayout wl{};
@@ -520,9 +526,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.work_counter2 = &sc->work_counter2;
     bl.overflow_list = c->b_list.as<int32_t>();
     bl.overflow_len = &sc->overflow_len;
-    bl.mid_list = c->b_list.as<int32_t>() + A;
-    bl.mid_len = &sc->mid_len;
-    bl.work_counter3 = &sc->work_counter3;
+    bl.dense_list = c->b_list.as<int32_t>() + A;
+    bl.dense_len = &sc->dense_len;
+    bl.dense_queue = &sc->dense_queue;
     bl.scratch = c->b_scratch.as<uint8_t>();
     bl.scratch_per_wave = spw;
     bl.clouds = clouds;
@@ -554,7 +560,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         pb.features = features ? features + 35 * c0 : nullptr;
         pb.counts = counts ? counts + 4 * c0 : nullptr;
         pb.pairs_out = pairs_out ? pairs_out + c0 * 3 * (int64_t)pair_cap * 2 : nullptr;
-        static_assert(offsetof(Scalars, work_counter3) - offsetof(Scalars, work_counter) == 8 * sizeof(uint32_t),
+        static_assert(offsetof(Scalars, dense_queue) - offsetof(Scalars, work_counter) == 8 * sizeof(uint32_t),
                       "queue and list counters are contiguous");
         HIP_TRY(c, hipMemsetAsync(&sc->work_counter, 0, 9 * sizeof(uint32_t), c->stream));
         // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
@@ -566,39 +572,38 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots,
                                     max_points > 64 && !c16 ? &wl : nullptr, wide_waves, &fork));
             if (c16) {
-                HIP_TRY(c, hipMemcpyAsync(&c->host->s.wide_len, &sc->wide_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                          c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));
-                const int64_t nwide = c->host->s.wide_len;
-                const int64_t rstride = ((int64_t)max_points * (max_points - 1) / 2 + 63) / 64 * 64;
-                const int64_t slice =
-                    std::max<int64_t>(1, std::min<int64_t>(nwide, (int64_t(16) << 30) / (20 * rstride)));
-                const size_t tmp_bytes = betti_rank_temp_bytes(slice, rstride);
-                HIP_TRY(c, c->b_rank16.ensure(8 * (size_t)slice * rstride + tmp_bytes));
-                const int64_t nsl = (nwide + slice - 1) / slice;
-                HIP_TRY(c, c->b_rscal16.ensure(sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(nsl, 1)));
-                std::vector<uint32_t> lens((size_t)std::max<int64_t>(nsl, 1));
-                for (int64_t q = 0; q < nsl; ++q) lens[q] = (uint32_t)std::min<int64_t>(slice, nwide - q * slice);
-                uint32_t* sl = c->b_rscal16.as<uint32_t>();
-                HIP_TRY(c, hipMemsetAsync(sl, 0, sizeof(uint32_t) * 2 * (size_t)std::max<int64_t>(nsl, 1), c->stream));
-                for (int64_t q = 0; q < nsl; ++q)
-                    HIP_TRY(c, hipMemcpyAsync(sl + 2 * q, &lens[q], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-                uint32_t* codes = c->b_rank16.as<uint32_t>();
-                uint32_t* sorted = codes + slice * rstride;
-                for (int64_t q = 0; q < nsl; ++q) {
-                    BettiLaunch wb = pb;
-                    wb.wide_list = c->b_wlist.as<int32_t>() + q * slice;
-                    wb.wide_len = sl + 2 * q;
-                    wb.wide_queue = sl + 2 * q + 1;
-                    HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, wb.wide_list,
-                                                (int64_t)lens[q], rstride, codes, sorted, sorted + slice * rstride,
-                                                tmp_bytes));
-                    wb.rank_codes = codes;
-                    wb.rank_sorted = sorted;
-                    wb.rank_stride = rstride;
-                    HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, lens[q])));
+                // slices of the wide list sized on the host from an upper bound of its length (the
+                // count pass's census of 65..kWideRegular-point complexes, which the host already
+                // holds), their lengths derived on the device from the bucket pass's wide_len: no
+                // host read, no stream synchronization
+                const int64_t nwide = given ? cnt : std::min<int64_t>(cnt, nw().wide_atoms);
+                if (nwide > 0) {
+                    const int64_t rstride = ((int64_t)max_points * (max_points - 1) / 2 + 63) / 64 * 64;
+                    const int64_t slice = std::max<int64_t>(
+                        1, std::min<int64_t>({nwide, (int64_t(16) << 30) / (20 * rstride), INT32_MAX / rstride}));
+                    const size_t tmp_bytes = betti_rank_temp_bytes(slice, rstride);
+                    HIP_TRY(c, c->b_rank16.ensure(8 * (size_t)slice * rstride + tmp_bytes));
+                    const int64_t nsl = (nwide + slice - 1) / slice;
+                    HIP_TRY(c, c->b_rscal16.ensure(sizeof(uint32_t) * 2 * (size_t)nsl));
+                    uint32_t* sl = c->b_rscal16.as<uint32_t>();
+                    HIP_TRY(c, launch_slice_lengths(c->stream, &sc->wide_len, slice, nsl, sl));
+                    uint32_t* codes = c->b_rank16.as<uint32_t>();
+                    uint32_t* sorted = codes + slice * rstride;
+                    for (int64_t q = 0; q < nsl; ++q) {
+                        BettiLaunch wb = pb;
+                        wb.wide_list = c->b_wlist.as<int32_t>() + q * slice;
+                        wb.wide_len = sl + 2 * q;
+                        wb.wide_queue = sl + 2 * q + 1;
+                        const int64_t ub = std::min<int64_t>(slice, nwide - q * slice);
+                        HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, wb.wide_list, ub,
+                                                    rstride, codes, sorted, sorted + slice * rstride, tmp_bytes,
+                                                    wb.wide_len));
+                        wb.rank_codes = codes;
+                        wb.rank_sorted = sorted;
+                        wb.rank_stride = rstride;
+                        HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, ub)));
+                    }
                 }
-                HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope
             }
         }
         if (pb.force_retry) {
@@ -617,15 +622,27 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         // caps, ripser.cpp:514-1269): reduced again with the big wide layout
         const int nmax = std::max(max_points, 64);
         const bool coded = nmax > kWideRegular;
-        {
-            // Device-driven retry when a few big-layout waves fit a small budget (complexes of up to
-            // a few hundred points; the 5 A path): the launch reads the retry list's length on the
-            // device and its waves leave at once when nothing overflowed, so the pass never waits
-            // for the host. The workspace is kept (its tables restored by every reduction).
+        HIP_TRY(c, c->b_rlist2.ensure(sizeof(int32_t) * (size_t)A));
+        int32_t* cur = c->b_rlist.as<int32_t>();
+        int32_t* nxt = c->b_rlist2.as<int32_t>();
+        int64_t nretry = -1;
+        int grow0 = 0;
+        if (!coded && c->dbg_big_log2 == 0) {
+            // Device-driven retry (complexes of up to kWideRegular points: the 5 A and 10 A paths):
+            // the launch reads the retry list's length on the device and its waves leave at once when
+            // nothing overflowed, so the pass never waits for the host. Its workspace (first growth
+            // level, >= 8 waves) is kept for the context's lifetime, its tables restored by every
+            // reduction; it takes at most an eighth of the HBM that is free or already its own, and
+            // 32 GB (288 GB per MI355X).
             WideLayout big = betti_wide_layout(nmax, true);
-            const int64_t fit = (int64_t(4) << 30) / big.total;
-            const int64_t waves = std::min<int64_t>({fit, betti_wide_resident_waves(c->device, nmax), 64});
-            if (!coded && waves >= 8 && c->dbg_big_log2 == 0) {
+            if (c->big_budget == 0) {
+                size_t free_b = 0, total_b = 0;
+                if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+                c->big_budget = std::min<int64_t>(int64_t(32) << 30, ((int64_t)free_b + (int64_t)c->b_big.bytes) / 8);
+            }
+            const int64_t waves =
+                std::min<int64_t>({c->big_budget / big.total, betti_wide_resident_waves(c->device, nmax), 64});
+            if (waves >= 8) {
                 if (c->big_nmax != nmax || c->big_waves < waves) {
                     HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
                     big.base = c->b_big.as<uint8_t>();
@@ -637,38 +654,48 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 BettiLaunch rb = pb;
                 rb.rank_codes = nullptr;
                 rb.rank_sorted = nullptr;
-                rb.retry_list = nullptr;  // a second overflow is reported (DGN_ERR_CAPACITY)
-                rb.retry_len = nullptr;
+                // a complex that outgrows this level: the device entry points report DGN_ERR_CAPACITY
+                // at their next synchronizing call (no host read here); the host entry points list it
+                // for the growing levels below
+                rb.retry_list = async_report ? nullptr : nxt;
+                rb.retry_len = async_report ? nullptr : &sc->retry2_len;
                 rb.force_retry = 0;
                 rb.retried = bflags + kBFRetried;
                 rb.wide_list = c->b_rlist.as<int32_t>();
                 rb.wide_len = &sc->retry_len;
                 rb.wide_queue = &sc->retry_queue;
+                if (!async_report) HIP_TRY(c, hipMemsetAsync(&sc->retry2_len, 0, sizeof(uint32_t), c->stream));
                 {
                     TimedLaunch t(c, "betti_retry", 0.0, 0.0);
                     HIP_TRY(c, launch_betti_wide(c->stream, rb, big, (int)waves));
                 }
                 HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
-                return DGN_OK;
+                if (async_report) return DGN_OK;
+                HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry2_len, &sc->retry2_len, sizeof(uint32_t),
+                                          hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                nretry = c->host->s.retry2_len;
+                if (nretry == 0) return DGN_OK;
+                std::swap(cur, nxt);
+                grow0 = 1;
             }
         }
-        // larger complexes: the retry workspace is sized by the number of complexes that overflowed
-        // (one host read of the list length)
-        HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                  c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        int64_t nretry = c->host->s.retry_len;
-        if (nretry == 0) return DGN_OK;
+        if (nretry < 0) {
+            // larger complexes: the retry workspace is sized by the number of complexes that
+            // overflowed (one host read of the list length)
+            HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            nretry = c->host->s.retry_len;
+            if (nretry == 0) return DGN_OK;
+        }
         // complexes above kWideRegular points (listed by the bucket pass) run on rank codes
         // (betti_rank_codes, the BIG / HUGE instantiations), in slices of at most 512 complexes.
         // The tables grow with the complexes (the reference's Ripser has no caps): a complex that
         // outgrows level `grow` is listed again and reduced at the next level, 4x the tables
         c->big_nmax = 0;  // the workspace below is laid out per call
-        HIP_TRY(c, c->b_rlist2.ensure(sizeof(int32_t) * (size_t)A));
-        int32_t* cur = c->b_rlist.as<int32_t>();
-        int32_t* nxt = c->b_rlist2.as<int32_t>();
         const int64_t rstride = ((int64_t)nmax * (nmax - 1) / 2 + 63) / 64 * 64;
-        for (int grow = 0;; ++grow) {
+        for (int grow = grow0;; ++grow) {
             const bool last = grow == kWideMaxGrow;
             WideLayout big = betti_wide_layout(nmax, true, 0, grow, c->dbg_big_log2 ? c->dbg_big_log2 : 24);
             size_t free_b = 0, total_b = 0;

@@ -55,17 +55,19 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
                                   int32_t* atom_struct, int32_t* cell_start, double4* cell_pos, double* weight,
                                   uint32_t* error_flag);
 // per-atom hit counts m (every neighbour within rc; the emit keeps min(m, kmax)); per block:
-// block_sums[b] = sum of min(m, kmax) and block_aux[4b] = max m, block_aux[4b+1] = sum over atoms
-// of (m + 1)^2, block_aux[4b+2] = largest structure, block_aux[4b+3] = sum of m;
+// block_sums[b] = sum of min(m, kmax) and block_aux[kAux b] = max m, block_aux[kAux b+1] = sum over
+// atoms of (m + 1)^2, block_aux[kAux b+2] = largest structure, block_aux[kAux b+3] = sum of m,
+// block_aux[kAux b+4] = atoms with 64 < m + 1 <= kWideRegular (low word) / > kWideRegular (high);
 // mask_out (optional) [A][kMaskWords]: exact hits of staged one-image structures.
 // defer [nblocks] (optional, needs mask_out): the one-image count kernel runs first and flags the
 // tiles it cannot count for the general kernel
+constexpr int kAux = 5;                   // block_aux words per count tile
 constexpr int64_t kCountListGrid = 2048;  // blocks of the general count launch over the flags
 hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* counts, int64_t* block_sums,
                               uint64_t* block_aux, uint64_t* mask_out, uint8_t* defer = nullptr);
 hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t* block_aux, int64_t nblocks,
                              int64_t* total, uint32_t* max_candidates, unsigned long long* sum_sq,
-                             uint32_t* max_natoms, unsigned long long* sum_m);
+                             uint32_t* max_natoms, unsigned long long* sum_m, unsigned long long* wide_atoms);
 // Fused emit: each block re-runs the search for its atoms, ranks, writes row_ptr / col / dist /
 // disp and the RBF. cap = graph_emit_cap(max candidates of the count pass, kmax): 64..2048 (the
 // per-wave hit lists in LDS) or kEmitGlobalKeys (rows of more candidates: key_rows, caller-owned,
@@ -107,10 +109,11 @@ struct BettiLaunch {
     // on the low-occupancy instantiation)
     int32_t* overflow_list;   // [num_atoms]
     uint32_t* overflow_len;
-    // 45..48-point complexes (NP = 48 launch after the NP = 44 main launch)
-    int32_t* mid_list;        // [num_atoms]
-    uint32_t* mid_len;
-    uint32_t* work_counter3;  // persistent work queue (mid launch)
+    // complexes of the main launch with more than 512 distances <= thr (its register sort holds
+    // 512 keys): listed by the main kernel and reduced by an NP = 64 launch after it
+    int32_t* dense_list;      // [num_atoms]
+    uint32_t* dense_len;
+    uint32_t* dense_queue;
     uint8_t* scratch;         // per-wave global scratch
     int64_t scratch_per_wave;
     // optional cloud-input mode (dgn_host_persistence): complex c = clouds[c][max_points][3]
@@ -156,6 +159,7 @@ constexpr int kWideBigPoints = 1024;
 constexpr int kWideRegular = 512;
 constexpr int kC16MaxPoints = 362;  // C(362, 2) < 2^16: u16 rank codes (wide launch)
 constexpr int kWideMaxGrow = 3;     // capacity-retry layout levels: tables of 2^24 .. 2^30 entries
+constexpr int64_t kWideMaxCols = int64_t(1) << 29;  // column / pivot / pair tables (pivot hash: 2x)
 constexpr int kWideWaves = 2;       // waves per wide workgroup, sharing one LDS adjacency buffer
 struct WideLayout {
     uint8_t* base;  // scratch of wave w at base + w * total
@@ -176,11 +180,15 @@ int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // devic
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
 // occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
 // equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,
-// size from betti_rank_temp_bytes.
+// size from betti_rank_temp_bytes. dev_len (may be null): the list's length on the device when
+// `count` is only an upper bound (slots at or past it are left empty).
 size_t betti_rank_temp_bytes(int64_t count, int64_t stride);
 hipError_t betti_rank_codes(hipStream_t s, const float* lower, int64_t tri_stride, const int32_t* npoints,
                             const int32_t* list, int64_t count, int64_t stride, uint32_t* codes, uint32_t* sorted,
-                            void* temp, size_t temp_bytes);
+                            void* temp, size_t temp_bytes, const uint32_t* dev_len = nullptr);
+// per slice q < nsl of a list of *total entries (device): sl[2q] = min(slice, max(0, *total - q slice)),
+// sl[2q + 1] = 0 (the slice launch's queue)
+hipError_t launch_slice_lengths(hipStream_t s, const uint32_t* total, int64_t slice, int64_t nsl, uint32_t* sl);
 
 // distance pass over complexes [first, first + count) of a BettiLaunch's cloud input
 struct DistLaunch {

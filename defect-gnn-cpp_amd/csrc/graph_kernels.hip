@@ -997,13 +997,18 @@ struct CountTileOut {
     DGN_LDS int32_t* nw;             // [qa] mask words per query (0: no mask)
     DGN_LDS uint64_t (*mask)[kMaskWords];
     DGN_LDS int64_t* wsum;           // [kW] per-wave sums ...
-    DGN_LDS uint64_t *wmax, *wsq, *wnat, *wm;
+    DGN_LDS uint64_t *wmax, *wsq, *wnat, *wm, *wwide;
 };
 struct CountAcc {
     int64_t sum = 0;
     uint32_t max = 0, nat = 0;
     uint64_t sq = 0, m = 0;
+    // local complexes of the Betti tiers past the narrow kernels (m + 1 points): 65..kWideRegular
+    // in the low word, above kWideRegular in the high word, so the host sizes those launches from
+    // the count it already reads back
+    uint64_t wide = 0;
     __device__ __forceinline__ void add(int m_, int natoms, uint64_t kmax) {
+        wide += m_ + 1 > kWideRegular ? (uint64_t(1) << 32) : (m_ + 1 > 64 ? 1u : 0u);
         sum += (uint64_t)m_ < kmax ? (int64_t)m_ : (int64_t)kmax;
         m += (uint64_t)m_;
         max = (uint32_t)m_ > max ? (uint32_t)m_ : max;
@@ -1024,6 +1029,7 @@ __device__ __forceinline__ void count_tile_store(const GraphLaunch& g, int64_t t
         o.wsq[w] = acc.sq;
         o.wnat[w] = acc.nat;
         o.wm[w] = acc.m;
+        o.wwide[w] = acc.wide;
     }
     __syncthreads();
     const int nq = (int)(g.num_atoms - g0 < qa ? g.num_atoms - g0 : qa);
@@ -1035,19 +1041,21 @@ __device__ __forceinline__ void count_tile_store(const GraphLaunch& g, int64_t t
         }
     if (threadIdx.x == 0) {
         int64_t s = 0;
-        uint64_t mx = 0, sq = 0, nat = 0, sm = 0;
+        uint64_t mx = 0, sq = 0, nat = 0, sm = 0, wd = 0;
         for (int k = 0; k < kW; ++k) {
             s += o.wsum[k];
+            wd += o.wwide[k];
             sm += o.wm[k];
             mx = o.wmax[k] > mx ? o.wmax[k] : mx;
             nat = o.wnat[k] > nat ? o.wnat[k] : nat;
             sq += o.wsq[k];
         }
         block_sums[tile] = s;
-        block_aux[4 * tile] = mx;
-        block_aux[4 * tile + 1] = sq;
-        block_aux[4 * tile + 2] = nat;
-        block_aux[4 * tile + 3] = sm;
+        block_aux[kAux * tile] = mx;
+        block_aux[kAux * tile + 1] = sq;
+        block_aux[kAux * tile + 2] = nat;
+        block_aux[kAux * tile + 3] = sm;
+        block_aux[kAux * tile + 4] = wd;
     }
 }
 
@@ -1055,9 +1063,9 @@ __device__ __forceinline__ void count_tile_store(const GraphLaunch& g, int64_t t
     __shared__ int32_t cnt_s[kQA], nw_s[kQA]; /* block outputs, written at the end */    \
     __shared__ uint64_t mask_s[kQA][kMaskWords];                                         \
     __shared__ int64_t wsum[kW];                                                         \
-    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW], wm[kW];                             \
+    __shared__ uint64_t wmax[kW], wsq[kW], wnat[kW], wm[kW], wwide[kW];                  \
     const CountTileOut out{lds(cnt_s), lds(nw_s), reinterpret_cast<DGN_LDS uint64_t(*)[kMaskWords]>(lds(&mask_s[0][0])), \
-                           lds(wsum), lds(wmax), lds(wsq), lds(wnat), lds(wm)};
+                           lds(wsum), lds(wmax), lds(wsq), lds(wnat), lds(wm), lds(wwide)};
 
 __global__ __launch_bounds__(kGraphBlock) __attribute__((amdgpu_waves_per_eu(DGN_COUNT1_WAVES))) void graph_count_one_kernel(
     GraphLaunch g, int32_t* __restrict__ counts, int64_t* __restrict__ block_sums, uint64_t* __restrict__ block_aux,
@@ -1189,20 +1197,22 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
                                                                   uint32_t* __restrict__ max_candidates,
                                                                   unsigned long long* __restrict__ sum_sq,
                                                                   uint32_t* __restrict__ max_natoms,
-                                                                  unsigned long long* __restrict__ sum_m) {
+                                                                  unsigned long long* __restrict__ sum_m,
+                                                                  unsigned long long* __restrict__ wide_atoms) {
     __shared__ int64_t wtot[kScanThreads / kWave];
     __shared__ uint64_t wmx[kScanThreads / kWave], wsq[kScanThreads / kWave], wna[kScanThreads / kWave],
-        wsm[kScanThreads / kWave];
+        wsm[kScanThreads / kWave], wwd[kScanThreads / kWave];
     const int tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
     __shared__ int64_t carry_s;
     if (tid == 0) carry_s = 0;
     // reductions of the block aux words: coalesced, independent loads
-    uint64_t mx = 0, sq = 0, na = 0, sm = 0;
+    uint64_t mx = 0, sq = 0, na = 0, sm = 0, wd = 0;
     for (int64_t i = tid; i < n; i += kScanThreads) {
-        mx = aux[4 * i] > mx ? aux[4 * i] : mx;
-        sq += aux[4 * i + 1];
-        na = aux[4 * i + 2] > na ? aux[4 * i + 2] : na;
-        sm += aux[4 * i + 3];
+        mx = aux[kAux * i] > mx ? aux[kAux * i] : mx;
+        sq += aux[kAux * i + 1];
+        na = aux[kAux * i + 2] > na ? aux[kAux * i + 2] : na;
+        sm += aux[kAux * i + 3];
+        wd += aux[kAux * i + 4];
     }
     __syncthreads();
     // exclusive scan, 8 consecutive sums per thread (two 32-byte loads per lane: coalesced), 8192
@@ -1243,16 +1253,19 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
     sq = wave_sum(sq);
     na = wave_max(na);
     sm = wave_sum(sm);
+    wd = wave_sum(wd);
     if (lane == 0) {
         wmx[w] = mx;
         wsq[w] = sq;
         wna[w] = na;
         wsm[w] = sm;
+        wwd[w] = wd;
     }
     __syncthreads();
     if (tid == 0) {
-        uint64_t m = 0, s = 0, a = 0, t = 0;
+        uint64_t m = 0, s = 0, a = 0, t = 0, x = 0;
         for (int k = 0; k < kScanThreads / kWave; ++k) {
+            x += wwd[k];
             m = wmx[k] > m ? wmx[k] : m;
             s += wsq[k];
             a = wna[k] > a ? wna[k] : a;
@@ -1262,6 +1275,7 @@ __global__ __launch_bounds__(kScanThreads) void block_scan_kernel(int64_t* __res
         *sum_sq = s;
         *max_natoms = (uint32_t)a;
         *sum_m = t;
+        *wide_atoms = x;
     }
 }
 
@@ -2100,9 +2114,9 @@ hipError_t launch_graph_count(hipStream_t s, const GraphLaunch& g, int32_t* coun
 
 hipError_t launch_block_scan(hipStream_t s, int64_t* v, const uint64_t* aux, int64_t n, int64_t* total,
                              uint32_t* max_candidates, unsigned long long* sum_sq, uint32_t* max_natoms,
-                             unsigned long long* sum_m) {
+                             unsigned long long* sum_m, unsigned long long* wide_atoms) {
     hipLaunchKernelGGL(block_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, v, aux, n, total, max_candidates,
-                       sum_sq, max_natoms, sum_m);
+                       sum_sq, max_natoms, sum_m, wide_atoms);
     return hipGetLastError();
 }
 

@@ -234,3 +234,29 @@ def test_betti_dist_triangles_fcc256(ctx):
         got, mapped, _, _ = _kernel_vs_reference_triangles(lower[gi], npts[gi], keys[gi], batch["lattice"][s],
                                                            batch["positions"][s * n:(s + 1) * n], a, 5.0)
         assert np.array_equal(got.view(np.uint32), mapped.view(np.uint32)), gi
+
+
+def test_rank_code_tiers_dense_complexes(ctx):
+    """The narrow kernels rank the distances <= thr of a complex in registers (512 keys in the
+    32/48-point tiers, 1,024 in the 64-point tier): denser complexes take the dense launch (NP = 64
+    after the main one) or the capacity retry (wide kernel). Clouds in a ball of radius thr/2 (every
+    pair within thr), some with exact ties, across every route; pairs bit-exact vs the oracle."""
+    rng = np.random.default_rng(21)
+    thr = 2.0
+    sizes = [12, 31, 33, 40, 46, 48, 52, 60, 64]
+    maxp = max(sizes)
+    clouds = np.zeros((2 * len(sizes), maxp, 3))
+    npts = np.array(sizes * 2, np.int32)
+    for c, n in enumerate(npts):
+        d = rng.normal(size=(n, 3))
+        d *= (rng.uniform(0, 1, (n, 1)) ** (1 / 3)) / np.linalg.norm(d, axis=1, keepdims=True)
+        pts = d * (thr / 2 * 0.999)
+        if c >= len(sizes):  # exact ties: a coarse grid inside the same ball
+            pts = np.round(pts * 2) / 2
+        clouds[c, :n] = pts
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=4096)
+    for c, n in enumerate(npts):
+        r = O.persistence(O.local_distances(clouds[c, :n]), n, np.float32(thr))
+        assert counts[c, 1] == r["n_inf0"], c
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
