@@ -13,7 +13,7 @@
 //     occurrence among the complex's sorted distances <= thr; 0xFFFF above thr and on the
 //     diagonal): order and equality are all the reduction ever asks of a distance
 //     (ripser.cpp:318-324, 386-395), the f32 values come back from the sorted table only for
-//     the emitted pairs. 2 B per entry keep a 48-point complex in 5 KB of LDS (six waves per
+//     the emitted pairs. 2 B per entry keep a 48-point complex in 5 KB of LDS (eight waves per
 //     SIMD instead of five with the f32 matrix);
 //   * distance matrix: the K=3 Gram product is built on the matrix cores with
 //     v_mfma_f64_16x16x4_f64 as three rank-1 products (exactly round(x_ik*x_jk) each), summed on
@@ -108,10 +108,10 @@ struct ScratchLayout {
 };
 
 // Per-wave LDS: the u16 rank-code matrix, the adjacency masks and the forest. The 48-point tier
-// (every 5 A complex of FCC-256: 43..46 points) takes 5,040 B, so LDS admits 32 waves per CU and
-// the register budget of six waves per SIMD (80 VGPRs, <= 106 SGPRs) binds; the f32 matrix took
-// 8 KB at 44 points (five waves per SIMD) and 9.6 KB at 48 (four). The hot reads (rows a, b, c
-// at column k = lane) are conflict-free (two lanes per bank word).
+// (every 5 A complex of FCC-256: 43..46 points) takes 5,040 B, so LDS admits 32 waves per CU (eight
+// per SIMD, the most the SIMD holds; the registers are then capped at 64 VGPRs / 80 SGPRs); the
+// f32 matrix took 8 KB at 44 points (five waves per SIMD) and 9.6 KB at 48 (four). The hot reads
+// (rows a, b, c at column k = lane) are conflict-free (two lanes per bank word).
 template <int NP>
 struct BettiSmem {
     static constexpr int S = NP;
@@ -119,8 +119,13 @@ struct BettiSmem {
     uint64_t adj[NP];
     uint8_t par[NP];                  // minimum spanning forest: parent of each vertex (0xFF = root)
 };
+#ifndef DGN_NARROW_WAVES
+#define DGN_NARROW_WAVES 8  // waves per SIMD of the 32- and 48-point tiers (A/B: 6 / 7 / 8 waves =
+                            // 139.4 / 132.8 / 130.1 ms betti_vr per config-4 shard; at 8 the compiler
+                            // spills a few per-complex values, none in the reduction's loops)
+#endif
 template <int NP>
-constexpr int betti_waves_per_simd() { return NP <= 48 ? 6 : 4; }
+constexpr int betti_waves_per_simd() { return NP <= 48 ? DGN_NARROW_WAVES : 4; }
 
 // ---------------------------------------------------------------------------------------
 // small helpers
@@ -1537,7 +1542,7 @@ static hipError_t launch_for(int np, hipStream_t st, const BettiLaunch& b, int g
 }
 
 // Tiered dispatch: the main launch uses the instantiation sized for typical complexes (NP = 48:
-// 24 resident waves per CU); complexes above it are listed by betti_bucket_kernel and reduced by
+// 32 resident waves per CU); complexes above it are listed by betti_bucket_kernel and reduced by
 // an NP = 64 launch (49..64 points) forked beside the main one and betti_wide_kernel (65..512
 // points). Counters and list lengths live on the device, so nothing synchronizes with the host in
 // between.

@@ -132,6 +132,7 @@ struct dgn_ctx {
     DevBuf bflags;                // [kBFWords] sticky Betti words (above)
     int big_nmax = 0, big_waves = 0;  // capacity-retry workspace (b_big) the tables were initialised for
     int64_t big_budget = 0;           // bytes the device-driven retry workspace may take (first use)
+    int64_t host_syncs = 0;           // host waits on the stream (dgn_debug_host_syncs)
     // betti workspace
     DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_rlist2, b_big, b_rank, b_rscal, b_rank16,
         b_rscal16;
@@ -172,6 +173,11 @@ int fail(dgn_ctx* c, int status, const std::string& msg) {
 }
 int hip_fail(dgn_ctx* c, hipError_t e, const char* where) {
     return fail(c, DGN_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+// every wait of the host for the context's stream goes through here (dgn_debug_host_syncs)
+hipError_t stream_sync(dgn_ctx* c) {
+    ++c->host_syncs;
+    return hipStreamSynchronize(c->stream);
 }
 #define HIP_TRY(ctx, expr)                                      \
     do {                                                        \
@@ -355,7 +361,7 @@ int graph_count_impl(dgn_ctx* c, const dgn_batch* b, double rc, uint64_t kmax, d
                                      &sc->total, &sc->max_candidates, &sc->sum_sq, &sc->max_natoms, &sc->sum_m, &sc->wide_atoms));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->s, sc, sizeof(Scalars), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     int st = take_flags(c);
     if (st) return st;
     if (c->host->s.graph_flag & kGErrFar)
@@ -422,7 +428,7 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
 }
 
 int check_emit_flag(dgn_ctx* c) {
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     return take_flags(c);
 }
 
@@ -616,7 +622,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             HIP_TRY(c, hipMemcpyAsync(c->b_rlist.p, all.data(), sizeof(int32_t) * (size_t)cnt, hipMemcpyHostToDevice,
                                       c->stream));
             HIP_TRY(c, hipMemcpyAsync(&sc->retry_len, &n32, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            HIP_TRY(c, stream_sync(c));
         }
         // complexes whose reduction outgrew a kernel's workspace (the reference's Ripser has no
         // caps, ripser.cpp:514-1269): reduced again with the big wide layout
@@ -641,7 +647,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 c->big_budget = std::min<int64_t>(int64_t(32) << 30, ((int64_t)free_b + (int64_t)c->b_big.bytes) / 8);
             }
             const int64_t waves =
-                std::min<int64_t>({c->big_budget / big.total, betti_wide_resident_waves(c->device, nmax), 64});
+                std::min<int64_t>({c->big_budget / big.total, betti_wide_resident_waves(c->device, nmax), 32});
             if (waves >= 8) {
                 if (c->big_nmax != nmax || c->big_waves < waves) {
                     HIP_TRY(c, c->b_big.ensure((size_t)big.total * (size_t)waves));
@@ -673,7 +679,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 if (async_report) return DGN_OK;
                 HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry2_len, &sc->retry2_len, sizeof(uint32_t),
                                           hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                HIP_TRY(c, stream_sync(c));
                 nretry = c->host->s.retry2_len;
                 if (nretry == 0) return DGN_OK;
                 std::swap(cur, nxt);
@@ -685,7 +691,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             // overflowed (one host read of the list length)
             HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, &sc->retry_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
+            HIP_TRY(c, stream_sync(c));
             nretry = c->host->s.retry_len;
             if (nretry == 0) return DGN_OK;
         }
@@ -750,14 +756,14 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             }
             HIP_TRY(c, hipMemcpyAsync(&c->host->s.retry_len, next_len, sizeof(uint32_t), hipMemcpyDeviceToHost,
                                       c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // `lens` leaves scope; the next level's count
+            HIP_TRY(c, stream_sync(c));  // `lens` leaves scope; the next level's count
             nretry = last ? 0 : c->host->s.retry_len;
             if (nretry == 0) break;
             std::swap(cur, nxt);
         }
         // the regular wide layout's tables are not touched; the big buffer is kept for reuse
         HIP_TRY(c, hipMemsetAsync(&sc->retry_len, 0, 2 * sizeof(uint32_t), c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_sync(c));
         return DGN_OK;
     };
     // triangles: floats per complex, padded to a multiple of 4 (16-byte aligned complexes)
@@ -811,7 +817,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     async_report = false;
 #endif
     if (async_report) return DGN_OK;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
 #ifdef DGN_PHASE_TIMING
     HIP_TRY(c, hipMemcpy(c->phase_host, c->phase.p, sizeof(c->phase_host), hipMemcpyDeviceToHost));
 #endif
@@ -910,7 +916,7 @@ int dgn_ctx_set_stream(dgn_ctx* c, void* s) {
     // a graph emit's consistency flag is still being copied on the old stream: let it land before
     // the stream is swapped, so the next synchronizing call reads it (take_emit_flag syncs only
     // the current stream)
-    if (c->emit_pending || c->betti_pending) HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->emit_pending || c->betti_pending) HIP_TRY(c, stream_sync(c));
     // NULL (the legacy null stream, e.g. torch's default stream) -> the context's own blocking
     // stream, which the null stream orders against; anything else is used as given
     c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
@@ -931,7 +937,7 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
 
 int dgn_ctx_synchronize(dgn_ctx* c) {
     if (!c) return DGN_ERR_ARG;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     return take_flags(c);  // a pending graph-emit or Betti failure surfaces here
 }
 
@@ -943,10 +949,17 @@ int dgn_debug_retry_count(dgn_ctx* c, int64_t* out) {
     HIP_TRY(c, hipMemcpyAsync(&c->host->pad, c->bflags.as<uint32_t>() + kBFRetried, sizeof(uint32_t),
                               hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemsetAsync(c->bflags.as<uint32_t>() + kBFRetried, 0, sizeof(uint32_t), c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     v = c->host->pad;
     *out = v;
     return take_flags(c);
+}
+
+int dgn_debug_host_syncs(dgn_ctx* c, int64_t* out) {
+    if (!c || !out) return DGN_ERR_ARG;
+    *out = c->host_syncs;
+    c->host_syncs = 0;
+    return DGN_OK;
 }
 
 const char* dgn_ctx_last_error(const dgn_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
@@ -1131,7 +1144,7 @@ int dgn_dev_node_features(dgn_ctx* c, const dgn_batch* b, const double* embed, i
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->s.error_flag, &sc->error_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
                               c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     if (c->host->s.error_flag)
         return fail(c, DGN_ERR_ARG, "dgn_dev_node_features: a species key has no embedding row (atom_embeddings.at)");
     return DGN_OK;
@@ -1185,7 +1198,7 @@ int dgn_host_edge_arrays(dgn_ctx* c, const dgn_batch* h, double r_cutoff, uint64
     if ((st = dgn_dev_edge_arrays(c, &d, rp.as<int64_t>(), col.as<int32_t>(), dist.as<double>(), disp.as<double>(),
                                   src.as<int32_t>(), tgt.as<int32_t>(), d32.as<float>(), p32.as<float>())))
         return st;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     dgn_edge_arrays* r = new dgn_edge_arrays();
     r->num_edges = E;
     r->sources = new int32_t[Em];
@@ -1275,7 +1288,7 @@ int dgn_debug_betti_clouds(dgn_ctx* c, const dgn_batch* h, double rc, int64_t fi
                                         max_points));
     HIP_TRY(c, hipMemcpyAsync(&c->host->s.graph_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost,
                               c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     if (c->host->s.graph_flag)
         return fail(c, DGN_ERR_INTERNAL, "dgn_debug_betti_clouds: search disagreed with the count pass");
     std::vector<float> tmp((size_t)(count * tri_stride));
@@ -1362,7 +1375,7 @@ int dgn_host_rbf(dgn_ctx* c, const double* distances, int64_t E, double rbf_cuto
         HIP_TRY(c, launch_rbf(c->stream, dd.as<double>(), E, rs, layout, dout.p));
     }
     HIP_TRY(c, hipMemcpyAsync(out, dout.p, elem * (size_t)E * rs.nbins, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_sync(c));
     return DGN_OK;
 }
 

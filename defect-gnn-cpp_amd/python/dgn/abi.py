@@ -24,6 +24,7 @@ EXPORTS = [
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug", "dgn_debug_retry_count",
+    "dgn_debug_host_syncs",
 ]
 DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2 = 1, 2, 3, 4, 6
 
@@ -101,6 +102,8 @@ def lib():
         L.dgn_ctx_set_debug.argtypes = [vp, C.c_int, C.c_int]
     if hasattr(L, "dgn_debug_retry_count"):
         L.dgn_debug_retry_count.argtypes = [vp, C.POINTER(i64)]
+    if hasattr(L, "dgn_debug_host_syncs"):
+        L.dgn_debug_host_syncs.argtypes = [vp, C.POINTER(i64)]
     L.dgn_ctx_last_error.restype = C.c_char_p
     L.dgn_ctx_last_error.argtypes = [vp]
     L.dgn_ctx_enable_timing.argtypes = [vp, C.c_int]
@@ -220,6 +223,12 @@ class Context:
         """Complexes the capacity-retry launches reduced since the last call (synchronizes)."""
         n = C.c_int64()
         self._check(lib().dgn_debug_retry_count(self.h, C.byref(n)), "retry_count")
+        return n.value
+
+    def host_syncs(self) -> int:
+        """Host waits on the context's stream since the last call (no synchronization itself)."""
+        n = C.c_int64()
+        self._check(lib().dgn_debug_host_syncs(self.h, C.byref(n)), "host_syncs")
         return n.value
 
     def synchronize(self):

@@ -45,10 +45,11 @@ typedef struct dgn_ctx dgn_ctx;
 
 /* A context owns its device workspaces, grown on demand and kept until dgn_ctx_destroy. The first
  * Betti pass with complexes of at most kWideRegular (512) points also allocates the device-driven
- * capacity-retry workspace once: up to 64 big-layout waves within a fixed 4 GB budget (about 4 GB at
- * 64 points), whether or not any complex overflows, so that later passes never wait for the host;
- * several contexts on one GPU each hold their own. Per-wave Betti scratch (narrow kernel ~1 MB per
- * resident wave, wide kernel 15-60 MB per wave, at most half of the free HBM) is held the same way. */
+ * capacity-retry workspace once: 8..32 first-level big-layout waves within an eighth of the free HBM
+ * and at most 32 GB (about 0.3 GB at 64 points, about 13 GB at the 10 A cutoff's ~340 points),
+ * whether or not any complex overflows, so that later passes never wait for the host; several
+ * contexts on one GPU each hold their own. Per-wave Betti scratch (narrow kernel ~1 MB per resident
+ * wave, wide kernel 15-60 MB per wave, at most half of the free HBM) is held the same way. */
 int dgn_ctx_create(int device, dgn_ctx** out);
 void dgn_ctx_destroy(dgn_ctx* ctx);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = the context's own. */
@@ -76,6 +77,9 @@ enum {
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 /* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */
 int dgn_debug_retry_count(dgn_ctx* ctx, int64_t* count);
+/* Diagnostics: how many times the context's calls waited for its stream since the last call
+ * (no synchronization itself; tests of the asynchronous device entry points). */
+int dgn_debug_host_syncs(dgn_ctx* ctx, int64_t* count);
 const char* dgn_ctx_last_error(const dgn_ctx* ctx);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream around every launch. */
@@ -181,11 +185,13 @@ int dgn_dev_betti(dgn_ctx* ctx, const dgn_batch* batch, const dgn_betti_params* 
 int dgn_host_betti(dgn_ctx* ctx, const dgn_batch* host_batch, const dgn_betti_params* p,
                    double* features, int32_t* counts);
 
-/* Fused step (device; no host synchronization while every local complex has at most 64 points, the
- * 5 A path: the capacity-retry launch is device-driven. Complexes of 65..362 points (the wide tier,
- * e.g. the reference's 10 A default) wait for the host twice: one read of the wide list's length for
- * the rank-code slices and one of the retry list's length to size the retry workspace. Errors are
- * reported by the next synchronizing call as for dgn_dev_betti): dgn_dev_graph_emit of a
+/* Fused step (device; no host synchronization while every local complex has at most kWideRegular
+ * (512) points -- the 5 A path and the reference's 10 A default alike: the wide tier's rank-code
+ * slices are sized from the count pass's census of wide complexes and take their lengths on the
+ * device, and the capacity-retry launch is device-driven (a complex that outgrows its first level
+ * is reported as DGN_ERR_CAPACITY here; dgn_host_betti grows the tables instead). Larger complexes
+ * size the rank-coded retry from a host read. Errors are reported by the next synchronizing call
+ * as for dgn_dev_betti): dgn_dev_graph_emit of a
  * preceding dgn_dev_graph_count, then dgn_dev_betti on the same batch. When the Betti cutoff equals
  * the graph cutoff (and epsilon is the default 1e-10) the Betti pass reuses the graph count's
  * per-atom neighbour counts and hit masks instead of searching a third time: CrystalGraph's
