@@ -47,29 +47,11 @@ $(LIB): $(KOBJS)
 oracle:
 	$(MAKE) -C oracle
 
-# diagnostics variant: per-phase cycle stamps in the Betti kernel (never used by bench/tests).
-#   make diag [DIAGTAG=x DIAGFLAGS=-DSOMETHING] -> lib/libdgn_diag[_x].so
-DIAGTAG   ?=
-DIAGFLAGS ?=
-DSUF   := $(if $(DIAGTAG),_$(DIAGTAG),)
-DBUILD := $(PKG)/build_diag$(DSUF)
-DIAG   := $(PKG)/lib/libdgn_diag$(DSUF).so
-diag: $(DIAG)
-$(DBUILD)/%.o: $(CSRC)/%.hip $(CSRC)/dgn_device.hpp $(CSRC)/dgn_internal.hpp
-	@mkdir -p $(DBUILD)
-	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -c $< -o $@
-$(DBUILD)/dgn_api.o: $(CSRC)/dgn_api.cpp include/dgn.h $(CSRC)/dgn_internal.hpp $(CSRC)/dgn_device.hpp
-	@mkdir -p $(DBUILD)
-	$(HIPCC) $(HIPFLAGS) -DDGN_PHASE_TIMING $(DIAGFLAGS) -x hip -c $< -o $@
-$(DIAG): $(DBUILD)/graph_kernels.o $(DBUILD)/betti_kernels.o $(DBUILD)/betti_wide.o $(DBUILD)/betti_rank.o $(DBUILD)/node_kernels.o $(DBUILD)/dgn_api.o
-	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
-
 clean:
-	rm -rf $(BUILD) $(SAN) $(LIB) $(PKG)/build_diag* $(PKG)/lib/libdgn_diag*.so $(FACADE) $(FBIN)
+	rm -rf $(BUILD) $(SAN) $(LIB) $(FACADE) $(FBIN)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean diag facade
+.PHONY: all oracle clean facade
 
 # Host-code sanitizer run (ASan + UBSan) over the CPU oracle and the facade's host-only code
 # (parser, Structure, PCA): builds build_san/san_check and runs it on the POSCAR fixtures.

@@ -73,7 +73,6 @@ constexpr uint32_t kErrNA = 1u << 2;
 constexpr uint32_t kErrPiv = 1u << 3;
 constexpr uint32_t kErrPairs = 1u << 4;
 constexpr uint32_t kErrR = 1u << 5;
-[[maybe_unused]] constexpr uint32_t kErrOrder = 1u << 6;  // -DDGN_ORDER_CHECK builds
 constexpr uint32_t kErrCapacity = kErrWorkCol | kErrNA | kErrPiv | kErrPairs | kErrR;
 
 // scratch layout per wave (bytes)
@@ -210,27 +209,6 @@ struct Complex {
     uint32_t err;
     // pair counts (wave-uniform)
     int n_d0, n_inf0, n_p1, n_p2;
-    int n_adds, n_spills;  // diagnostics
-#ifdef DGN_PHASE_TIMING
-    mutable uint32_t walk_steps = 0;  // min-cofacet walk steps of this lane (lane efficiency)
-    uint64_t* ph = nullptr;
-    uint64_t* tprev = nullptr;
-    int sdim = 0;  // dimension of the serial walk in progress (DGN_DIAG_DIM: count only that one)
-#ifndef DGN_DIAG_DIM
-#define DGN_DIAG_DIM 0
-#endif
-    __device__ bool tagged() const { return DGN_DIAG_DIM == 0 || sdim == 0 || sdim == DGN_DIAG_DIM; }
-    __device__ void stamp(int k) {
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        if (tagged()) ph[k] += t - *tprev;
-        *tprev = t;
-    }
-#define DGN_SUB(k) stamp(k)
-#else
-#define DGN_SUB(k) \
-    do {           \
-    } while (0)
-#endif
 
     // Distances are rank codes (order- and equality-preserving): maxima are unsigned maxima, and
     // a simplex through a pair above thr (or a repeated vertex) gets kNoCode by the maximum
@@ -293,9 +271,6 @@ struct Complex {
         uint64_t r = ((uint64_t)__builtin_bitreverse32((uint32_t)cand) << 32) | __builtin_bitreverse32((uint32_t)(cand >> 32));
         // four candidates per step (descending), their distance reads issued together
         for (int st = 0; r && st < steps; ++st) {
-#ifdef DGN_PHASE_TIMING
-            ++walk_steps;
-#endif
             int kk[4];
             bool val[4];
 #pragma unroll
@@ -535,9 +510,6 @@ struct Complex {
                 mult = __popcll(ballot(lmin == mt));
             }
             const uint64_t m = mt + base;
-#ifdef DGN_PHASE_TIMING
-            if (tagged()) { ph[24] += 1; ph[25] += (uint64_t)v; }
-#endif
             // no cofacet above floor: the minimum is a non-neighbour key (high word kNoCode; every
             // lane without a cofacet: all ones) or a wrapped key <= floor
             if ((uint32_t)(m >> 32) >= kNoCode || m <= floor) return kInf;
@@ -577,9 +549,6 @@ struct Complex {
     // initial pivot, all computed lane-parallel; larger sets are rank-sorted into scratch.
     __device__ void reduce_serial(int dim, int nna) {
         const int lane = lane_id();
-#ifdef DGN_PHASE_TIMING
-        sdim = dim;
-#endif
         if (nna > kNACap) { err |= kErrNA; return; }
         const uint64_t* gk = sp<uint64_t>(ScratchLayout::na_key);
         const uint64_t* gt = sp<uint64_t>(ScratchLayout::na_tau);
@@ -620,7 +589,6 @@ struct Complex {
             }
             __syncthreads();
         }
-        DGN_SUB(16);
         uint32_t* gvstore = sp<uint32_t>(ScratchLayout::vstore);
         int npiv = 0, vused = 0;
         for (int ci = 0; ci < nna; ++ci) {
@@ -653,15 +621,9 @@ struct Complex {
             tau = uni64(tau);
             const uint32_t cp = key_packed(colkey);
             const uint32_t birth = key_code(colkey);
-            DGN_SUB(17);
             int owner = (int)uni((uint32_t)find_pivot(npiv, tau));
-            DGN_SUB(18);
             uint32_t app = uni(owner >= 0 ? kNone : (have_app ? app0 : apparent_owner_wave(dim, tau)));
-            DGN_SUB(19);
             int v = 0;  // 0 = lazy: V == {this column}
-#ifdef DGN_PHASE_TIMING
-            if (tagged()) ph[27] += (owner < 0 && app == kNone) ? 1 : 0;  // settled by its initial pivot
-#endif
             if (owner >= 0 || app != kNone) {
                 v_toggle(dim, cp, v);
                 int guard = 0;
@@ -670,13 +632,9 @@ struct Complex {
                     bool ok = true;
                     if (app != kNone) {
                         // an apparent owner precedes this column in Ripser's order (key greater):
-                        // guaranteed (an apparent pair's column is the F-max facet of its pivot),
-                        // verified only in -DDGN_ORDER_CHECK builds (3 distance reads and a
-                        // branch on every apparent addition cost 2.4 % of the Betti pass); the
-                        // parity tests compare every pair with the oracle either way
-#ifdef DGN_ORDER_CHECK
-                        if (!(column_key(dim, app) > colkey)) { err |= kErrOrder; return; }
-#endif
+                        // guaranteed (an apparent pair's column is the F-max facet of its pivot);
+                        // checking it cost 2.4 % of the Betti pass, and the parity tests compare
+                        // every pair with the oracle
                         ok = v_toggle(dim, app, v);
                     } else {
                         const uint32_t m = piv_meta(owner);
@@ -695,28 +653,13 @@ struct Complex {
                         }
                     }
                     if (!ok) { err |= kErrWorkCol; return; }
-                    ++n_adds;
-                    DGN_SUB(20);
-#ifdef DGN_PHASE_TIMING
-                    if (tagged()) {
-                        ph[14] += (uint64_t)v;
-                        ph[15] += (uint64_t)v * (uint64_t)v;
-                        ph[23] = (uint64_t)v > ph[23] ? (uint64_t)v : ph[23];
-                    }
-#endif
                     tau = uni64(v > 0 ? pivot_of_V(dim, v, tau) : kInf);
-                    DGN_SUB(21);
                     if (tau == kInf) break;  // zero column: essential class, not emitted
                     owner = (int)uni((uint32_t)find_pivot(npiv, tau));
-                    DGN_SUB(18);
                     app = uni(owner >= 0 ? kNone : apparent_owner_wave(dim, tau));
-                    DGN_SUB(19);
                     if (owner < 0 && app == kNone) break;  // tau is this column's pivot
                     if (++guard > 100000) { err |= kErrWorkCol; return; }
                 }
-#ifdef DGN_PHASE_TIMING
-                if (tagged()) ph[28] += tau == kInf ? 1 : 0;
-#endif
                 if (tau == kInf) continue;  // zero column
             }
             // ---- tau is the pivot of this column ----
@@ -749,30 +692,10 @@ struct Complex {
             piv_push(npiv, tau, meta);
             npiv = (int)uni((uint32_t)(npiv + 1));
             lds_sync();
-            DGN_SUB(22);
         }
     }
 };
 
-#ifdef DGN_PHASE_TIMING
-#define DGN_PHASE(k)                                          \
-    do {                                                      \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
-        ph[k] += t_ - t_prev;                                 \
-        t_prev = t_;                                          \
-    } while (0)
-#else
-#define DGN_PHASE(k) \
-    do {             \
-    } while (0)
-#endif
-// VALU accounting builds only (-DDGN_STOP_AT=k): leave the complex after phase k
-#ifdef DGN_STOP_AT
-#define DGN_STOP(k) \
-    if (DGN_STOP_AT == (k)) { lds_sync(); continue; }
-#else
-#define DGN_STOP(k)
-#endif
 
 // Ascending bitonic sort of 64 R keys in registers, element e = lane * R + r: exchanges at a
 // distance j < R stay in the lane (registers r and r ^ j), the others pair lane with lane ^ (j / R)
@@ -947,12 +870,6 @@ __device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __
 template <int NP>
 __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kernel(BettiLaunch bl) {
     __shared__ BettiSmem<NP> s;
-#ifdef DGN_PHASE_TIMING
-    // diagnostics counters in LDS (registers would change the kernel's occupancy)
-    __shared__ uint64_t ph[32];
-    if (lane_id() < 32) ph[lane_id()] = 0;
-    uint64_t t_prev = __builtin_amdgcn_s_memtime();
-#endif
     // the lane index is re-derived opaquely at every phase (relane): the compiler cannot hoist
     // lane-derived masks and per-lane addresses out of the complex loop, where they were live
     // across the whole kernel and spilled (16 VGPRs at the 96-VGPR budget of NP = 44)
@@ -999,13 +916,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             // pointers, which the compiler then spills
             uint8_t* cscr = scratch;
             asm volatile("" : "+s"(cscr));
-            Complex<NP> cx{s, n, bl.thr, cscr, 0u, 0, 0, 0, 0, 0, 0};
+            Complex<NP> cx{s, n, bl.thr, cscr, 0u, 0, 0, 0, 0};
             cx.zero_code = 0xFFFFFFFFu;
-#ifdef DGN_PHASE_TIMING
-            cx.ph = ph;
-            cx.tprev = &t_prev;
-#endif
-            DGN_PHASE(7);
             constexpr int S = BettiSmem<NP>::S;
             cx.zero_code = rank_codes<NP>(s, bl.lower + gi * bl.tri_stride, n, cx.thr,
                                           cx.template sp<float>(ScratchLayout::svals),
@@ -1026,7 +938,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                 continue;
             }
             lds_sync();
-            DGN_PHASE(0); DGN_STOP(1)
             // ---- adjacency (sparse_distance_matrix: i != j and d <= thr, ripser.cpp:386-395) ----
             relane();
             uint64_t myadj = 0;  // this lane's row
@@ -1114,7 +1025,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
             __syncthreads();  // edge list (global scratch) visible to every lane
             cx.n_p1 = 0;
             cx.n_p2 = 0;
-            DGN_PHASE(1); DGN_STOP(2)
             uint64_t* na_key = cx.template sp<uint64_t>(ScratchLayout::na_key);
             uint64_t* na_tau = cx.template sp<uint64_t>(ScratchLayout::na_tau);
             uint8_t* mincof = cx.template sp<uint8_t>(ScratchLayout::mincof);
@@ -1186,17 +1096,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     }
                 }
                 __syncthreads();
-                DGN_PHASE(2); DGN_STOP(3)
-#ifdef DGN_PHASE_TIMING
-                ph[8] += nna;
-                const int a0 = cx.n_adds;
-#endif
                 cx.reduce_serial(1, nna);
                 __syncthreads();  // clearing marks (scratch stores) complete before the dim-2 pass
-                DGN_PHASE(3); DGN_STOP(4)
-#ifdef DGN_PHASE_TIMING
-                ph[10] += cx.n_adds - a0;
-#endif
             }
             if (!(dim_max >= 2 && cx.err == 0) && n >= 3) {
                 // no dim-2 pass to consume them: erase every triangle entry (clearing marks)
@@ -1258,7 +1159,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     }
                 }
                 __syncthreads();  // the list (scratch) is read by other lanes
-                DGN_PHASE(26); DGN_STOP(5)
                 // (2b) one lane per column (uncleared triangle), in two rounds as in the dim-1
                 // pass: round A walks at most kAppSteps steps per column and lists the unsettled
                 // ones, round B walks those to the end. Global reads leave the per-round dependency
@@ -1294,20 +1194,6 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                         }
                         if (!dfr) at(mincof, tri_dense_lane(a, b, c)) = (uint8_t)mc;
                     }
-#ifdef DGN_PHASE_TIMING
-                    // lane efficiency of the round-synchronous walk: steps summed over lanes [29],
-                    // the longest lane's steps [30], rounds [31]
-                    {
-                        const uint32_t st_ = cx.walk_steps;
-                        cx.walk_steps = 0;
-                        const uint64_t tot_ = wave_sum((uint64_t)st_), mx_ = wave_max((uint64_t)st_);
-                        if (lane == 0) {
-                            ph[29] += tot_;
-                            ph[30] += mx_;
-                            ph[31] += 1;
-                        }
-                    }
-#endif
                     const uint64_t bal = ballot(na_col);
                     if (na_col) {
                         const int slot = nna + mask_prefix(bal);
@@ -1346,19 +1232,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     }
                 }
                 __syncthreads();
-                DGN_PHASE(4); DGN_STOP(6)
-#ifdef DGN_PHASE_TIMING
-                ph[9] += nna;
-                const int a0 = cx.n_adds;
-#endif
                 cx.reduce_serial(2, nna);
                 lds_sync();
-                DGN_PHASE(5);
-#ifdef DGN_PHASE_TIMING
-                ph[11] += cx.n_adds - a0;
-                ph[12] += cx.n_spills;
-                ph[13] += 1;
-#endif
             }
             __syncthreads();
             if (cx.n_p1 > kPairCap || cx.n_p2 > kPairCap) cx.err |= kErrPairs;
@@ -1388,14 +1263,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
                     at(bl.counts + 4 * gi, lane) = lane == 0 ? cx.n_d0 : (lane == 1 ? cx.n_inf0 : (lane == 2 ? cx.n_p1 : cx.n_p2));
             }
             lds_sync();
-            DGN_PHASE(6);
         }
     }
-#ifdef DGN_PHASE_TIMING
-    if (lane == 0 && bl.phase_cycles)
-        for (int k = 0; k < 32; ++k) if (k != 23) atomicAdd(&bl.phase_cycles[k], (unsigned long long)ph[k]);
-    if (lane == 0 && bl.phase_cycles) atomicMax(&bl.phase_cycles[23], (unsigned long long)ph[23]);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------

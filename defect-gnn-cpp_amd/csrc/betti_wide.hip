@@ -140,9 +140,6 @@ struct WideCx {
     // mode): the reduction tests common neighbours from the distances alone (no adjacency), with
     // an all-ones diagonal excluding the simplex's own vertices
     uint32_t thrc = 0;
-#ifdef DGN_PHASE_TIMING
-    uint64_t dg_searches = 0, dg_floor_iters = 0;  // diagnostics: pivot searches and their floor rounds
-#endif
 
     __device__ float value(uint32_t dc) const { return CODED ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
 
@@ -480,9 +477,6 @@ struct WideCx {
         uint32_t ds = 0, dab = 0, dac = 0, dbc = 0, hda = 0, hdb = 0, hdc = 0;
         PT colp = 0;
         bool found = false;
-#ifdef DGN_PHASE_TIMING
-        uint64_t nsteps = 0, niter = 0, ncols = 0;
-#endif
         for (;;) {
             // (1) lanes without a triangle take the next ones from the cursor, in order
             for (;;) {
@@ -566,9 +560,6 @@ struct WideCx {
                     ds = max(max(dab, dac), dbc);
                     fresh = false;
                 }
-#ifdef DGN_PHASE_TIMING
-                nsteps += 1;
-#endif
                 bool done;
                 if (cleared) {
                     mc_t[tidx] = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
@@ -612,29 +603,12 @@ struct WideCx {
                         ntau = best;
                         ntv = bestp;
                         ncolp = colp;
-#ifdef DGN_PHASE_TIMING
-                        ncols += 1;
-#endif
                     }
                 }
                 if (done) act = false;
             }
             na_append(base, na, nna, colkey, ntau, ntv, ncolp);
-#ifdef DGN_PHASE_TIMING
-            niter += 1;
-#endif
         }
-#ifdef DGN_PHASE_TIMING
-        // walk steps: summed over lanes [26], wave iterations [27], columns walked [28]
-        if (bl.phase_cycles) {
-            const uint64_t tot = wave_sum(nsteps), cols = wave_sum(ncols);
-            if (lane == 0) {
-                atomicAdd(&bl.phase_cycles[26], (unsigned long long)tot);
-                atomicAdd(&bl.phase_cycles[27], (unsigned long long)niter);
-                atomicAdd(&bl.phase_cycles[28], (unsigned long long)cols);
-            }
-        }
-#endif
         wave_scratch_sync();
         return nna;
     }
@@ -876,13 +850,7 @@ struct WideCx {
         // readlane, so an entry costs no dependent load; the first 64 stay across floor rounds
         const PT vl0 = k < v ? ((VREG && !vspill) ? vreg : VL[k]) : PT(0);
         const uint32_t vd0 = k < v ? sdiam(dim, vl0) : 0u;
-#ifdef DGN_PHASE_TIMING
-        ++dg_searches;
-#endif
         for (;;) {
-#ifdef DGN_PHASE_TIMING
-            ++dg_floor_iters;
-#endif
             uint64_t lmin = kInfW, lp = 0;
             int lcnt = 0;
             auto eval = [&](PT s, uint32_t ds) {
@@ -973,28 +941,7 @@ struct WideCx {
             err |= kENA;
             return;
         }
-#ifdef DGN_PHASE_TIMING
-        // diagnostics build: sub-phase cycles of the reduction into phase_cycles[16..21],
-        // pivot-search iterations [24] and their V entries [25], column additions [26]
-        uint64_t sb[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        uint64_t tq = __builtin_amdgcn_s_memtime();
-        auto sub = [&](int k) {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            sb[k] += t - tq;
-            tq = t;
-        };
-#define WSUB(k) sub(k)
-#define WCNT(k, x) (sb[k] += (uint64_t)(x))
-#else
-#define WSUB(k) \
-    do {        \
-    } while (0)
-#define WCNT(k, x) \
-    do {           \
-    } while (0)
-#endif
         nna = sort_na(base, nna, dim == 2);
-        WSUB(0);
         const uint64_t* K = sp<uint64_t>(ly.na_key) + base;
         const uint64_t* T = sp<uint64_t>(ly.na_tau) + base;
         const uint64_t* V = sp<uint64_t>(ly.na_tv) + base;
@@ -1012,7 +959,6 @@ struct WideCx {
             const uint32_t birth = kdiam(colkey);
             PT app;
             uint64_t meta = lookup(dim, tau, tv, app);
-            WSUB(1);
             int v = 0;  // 0 = lazy: V == {this column}
             vspill = !VREG;
             if (meta != kNoMetaW || app != kNoneP) {
@@ -1037,14 +983,9 @@ struct WideCx {
                         err |= kEWork;
                         break;
                     }
-                    WSUB(3);
-                    WCNT(6, 1);
-                    WCNT(7, v);
                     tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInfW;
-                    WSUB(4);
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
                     meta = lookup(dim, tau, tv, app);
-                    WSUB(1);
                     if (meta == kNoMetaW && app == kNoneP) break;  // tau is this column's pivot
                     if (++guard > ly.guard) {
                         err |= kEGuard;
@@ -1089,21 +1030,8 @@ struct WideCx {
                 break;
             }
             ++npiv;
-            WSUB(5);
         }
         wave_scratch_sync();
-#ifdef DGN_PHASE_TIMING
-        if (lane == 0 && bl.phase_cycles) {
-            for (int k = 0; k < 6; ++k) atomicAdd(&bl.phase_cycles[16 + k], (unsigned long long)sb[k]);
-            atomicAdd(&bl.phase_cycles[24], (unsigned long long)sb[6]);
-            atomicAdd(&bl.phase_cycles[25], (unsigned long long)sb[7]);
-            atomicAdd(&bl.phase_cycles[29], (unsigned long long)dg_searches);
-            atomicAdd(&bl.phase_cycles[30], (unsigned long long)dg_floor_iters);
-            dg_searches = dg_floor_iters = 0;
-        }
-#endif
-#undef WSUB
-#undef WCNT
         // empty the pivot table for the next dimension / complex
         uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint32_t* used = sp<uint32_t>(ly.h_used);
@@ -1150,52 +1078,24 @@ struct WideCx {
         return true;
     }
 
-#ifdef DGN_PHASE_TIMING
-    // diagnostics build: cycles per phase into phase_cycles[0..7], column counts [8], [9]
-    uint64_t t0 = 0;
-    __device__ void stamp(int k) {
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        if (lane_id() == 0 && bl.phase_cycles && k >= 0) atomicAdd(&bl.phase_cycles[k], (unsigned long long)(t - t0));
-        t0 = t;
-    }
-#define WSTAMP(k) stamp(k)
-#else
-#define WSTAMP(k) \
-    do {          \
-    } while (0)
-#endif
     // Phase 1, with the workgroup's adjacency buffer held (betti_wide_body): the matrix and the
     // bitsets, the forest, the edge list and both lane-parallel (apparent) passes; the dim-2 pass
     // runs before the dim-1 reduction, so the columns the latter clears (their triangles are dim-1
     // pivots) are dropped from the dim-2 list when it is sorted
     int nna1 = 0, nna2 = 0, base2 = 0, ncl = 0;
     __device__ void apparent(int64_t gi, int64_t slot) {
-        WSTAMP(-1);
         load(gi, slot);
-        WSTAMP(0);
         prim();
         const int n_edges = edge_list();
-        WSTAMP(1);
         nna1 = pass_dim1(n_edges);
-        WSTAMP(2);
         base2 = pow2ceil(nna1);
         nna2 = pass_dim2(n_edges, base2);
-        WSTAMP(4);
-#ifdef DGN_PHASE_TIMING
-        if (lane_id() == 0 && bl.phase_cycles) {
-            atomicAdd(&bl.phase_cycles[8], (unsigned long long)nna1);
-            atomicAdd(&bl.phase_cycles[9], (unsigned long long)nna2);
-            atomicAdd(&bl.phase_cycles[10], (unsigned long long)n_edges);
-        }
-#endif
     }
     // Phase 2, from scratch alone (no LDS): the two reductions, the statistics and the outputs.
     // True when the complex's outputs were written.
     __device__ bool reduce_finish(int64_t gi, double weight) {
         reduce(1, nna1, 0);
-        WSTAMP(3);
         if (err == 0u) reduce(2, nna2, base2);
-        WSTAMP(5);
         // the dim-1 clearing marks were read by the dim-2 sort; reset them for the next complex
         // (every other min-cofacet entry a later complex reads is rewritten by its dim-2 pass)
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
@@ -1204,10 +1104,8 @@ struct WideCx {
         wave_scratch_sync();
         const bool ok = finish(gi, weight);
         wave_scratch_sync();
-        WSTAMP(6);
         return ok;
     }
-#undef WSTAMP
 };
 
 template <int KW, int MODE>

@@ -153,10 +153,6 @@ struct dgn_ctx {
     DevBuf h_lat, h_pos, h_spec, h_off;
     DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
     DevBuf emit_keys;     // the large-row emit's per-wave key rows (graph_emit_cap == kEmitGlobalKeys)
-#ifdef DGN_PHASE_TIMING
-    DevBuf phase;
-    unsigned long long phase_host[32] = {0};
-#endif
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -549,11 +545,6 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     bl.retry_list = c->b_rlist.as<int32_t>();
     bl.retry_len = &sc->retry_len;
     bl.force_retry = c->dbg_force_retry ? 1 : 0;  // tests only (dgn_ctx_set_debug)
-#ifdef DGN_PHASE_TIMING
-    HIP_TRY(c, c->phase.ensure(32 * sizeof(unsigned long long)));
-    HIP_TRY(c, hipMemsetAsync(c->phase.p, 0, 32 * sizeof(unsigned long long), c->stream));
-    bl.phase_cycles = c->phase.as<unsigned long long>();
-#endif
     // Betti pass over complexes [c0, c0 + cnt) whose triangles are in `lower`
     auto vr_pass = [&](int64_t c0, int64_t cnt, const float* tri, int64_t tri_stride, const int32_t* np,
                        const double* w, double bytes) -> int {
@@ -813,14 +804,8 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     // (asynchronous: the next synchronizing call reports them), the host ones wait and report
     HIP_TRY(c, hipMemcpyAsync(c->host->betti_flags, bflags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     c->betti_pending = true;
-#ifdef DGN_PHASE_TIMING
-    async_report = false;
-#endif
     if (async_report) return DGN_OK;
     HIP_TRY(c, stream_sync(c));
-#ifdef DGN_PHASE_TIMING
-    HIP_TRY(c, hipMemcpy(c->phase_host, c->phase.p, sizeof(c->phase_host), hipMemcpyDeviceToHost));
-#endif
     return take_flags(c);
 }
 
@@ -1379,14 +1364,6 @@ int dgn_host_rbf(dgn_ctx* c, const double* distances, int64_t E, double rbf_cuto
     return DGN_OK;
 }
 
-#ifdef DGN_PHASE_TIMING
-/* diagnostics build only (libdgn_diag.so): per-phase s_memtime cycles of the last Betti launch */
-int dgn_diag_phase_cycles(dgn_ctx* c, unsigned long long* out) {
-    if (!c || !out) return DGN_ERR_ARG;
-    std::memcpy(out, c->phase_host, sizeof(c->phase_host));
-    return DGN_OK;
-}
-#endif
 
 int64_t dgn_synth_atoms_per_structure(int kind, int m) {
     if (m <= 0) return -1;

@@ -128,7 +128,6 @@ struct BettiLaunch {
     // optional raw pair output: [C][3][pair_cap][2] f32 (dim0 as (0, death)), unsorted
     float* pairs_out;
     int32_t pair_cap;
-    unsigned long long* phase_cycles;  // [32] diagnostics build only (DGN_PHASE_TIMING)
     // complexes above 64 points, listed by the bucket pass for betti_wide_kernel
     int32_t* wide_list;       // [num_atoms]
     uint32_t* wide_len;

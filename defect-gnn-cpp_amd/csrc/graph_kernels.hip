@@ -1641,22 +1641,6 @@ __host__ __device__ inline EmitLayout emit_layout(int stage_cap, int cap, bool s
     return l;
 }
 
-// diagnostics build (-DDGN_EMIT_PHASES, never bench/tests): per-wave s_memtime cycles of the emit's
-// phases summed into dgn_emit_phase[] (read by dgn_diag_emit_phases)
-#ifdef DGN_EMIT_PHASES
-__device__ unsigned long long dgn_emit_phase[8];
-#define EMIT_STAMP(k)                                  \
-    do {                                               \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-        ph[k] += t_ - tprev;                           \
-        tprev = t_;                                    \
-    } while (0)
-#else
-#define EMIT_STAMP(k) \
-    do {              \
-    } while (0)
-#endif
-
 // the tiles (kQA atoms) of one emit launch: row tiles [row0, row0 + nrow) and RBF tiles
 // [rbf0, rbf0 + nrbf) whose rows an earlier launch wrote; fused: each row block streams its own
 // RBF after its rows (one launch, nrbf = 0)
@@ -1727,10 +1711,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
     const int qa = g.qa;
     const int64_t g0 = tile * qa;
     const int nq = (int)(g.num_atoms - g0 < qa ? g.num_atoms - g0 : qa);
-#ifdef DGN_EMIT_PHASES
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t tprev = __builtin_amdgcn_s_memtime();
-#endif
     // the RBF of this tile from its rows (row_ptr, dist), by the block's 4 waves; region A must be dead
     auto rbf_tile = [&](bool rows_in_lds) __attribute__((always_inline)) {
         for (int i = threadIdx.x; i <= ly.gm.h + 1; i += kGraphBlock) {
@@ -1754,15 +1734,10 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
         else
             rbf_stream_wave(reinterpret_cast<double*>(rbf) + e0 * rs.nbins, ne, dl, ctab,
                             reinterpret_cast<DGN_LDS double*>(base + ly.rbf + w * ly.wbytes), rs, ly.gm, w);
-        EMIT_STAMP(4);
     };
     if constexpr (STREAM) {
         if (is_rbf) {
             rbf_tile(false);
-#ifdef DGN_EMIT_PHASES
-            if (lane == 0 && (blockIdx.x & 63) == 1)
-                for (int k = 0; k < 8; ++k) atomicAdd(&dgn_emit_phase[k], (unsigned long long)ph[k]);
-#endif
             return;
         }
     }
@@ -1788,10 +1763,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             mask_s[a_ * nwm + wd] = g.mask[mask_index(g0 + a_, wd, qa)];
         }
     __syncthreads();
-    EMIT_STAMP(0);
     for_block_atoms(g, st, 0, g.num_atoms, tile, qa, [&](const StructMeta& M, const PosSrc& P, int64_t gi, int t, int64_t b)
                                                __attribute__((always_inline)) {
-        EMIT_STAMP(1);
         const int li = (int)(gi - M.first);
         double q[3];
         P.get(li, q);
@@ -1847,7 +1820,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
                 }
                 m += __popcll(bal);
             });
-        EMIT_STAMP(2);
         const int64_t rs0 = row_start[t];
         const int kept = (int)(row_start[t + 1] - rs0);
         if (m > cap || kept != (m < K ? m : K)) {
@@ -1885,7 +1857,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             rank_large(kd, kj, m, put);
         }
         key_rows_sync();
-        EMIT_STAMP(3);
         if constexpr (!STREAM) {
             // 3. this atom's RBF rows: kept x nbins contiguous values from rs0 * nbins
             if (rs.dtype != 0 && rbf) {
@@ -1904,10 +1875,6 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
             rbf_tile(true);
         }
     }
-#ifdef DGN_EMIT_PHASES
-    if (lane == 0 && (blockIdx.x & 63) == 0)  // sampled: 1 block in 64 (atomics on 8 words serialise)
-        for (int k = 0; k < 8; ++k) atomicAdd(&dgn_emit_phase[k], (unsigned long long)ph[k]);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2208,15 +2175,3 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
 
 }  // namespace dgn
 
-#ifdef DGN_EMIT_PHASES
-// diagnostics build only: read (and optionally clear) the emit phase cycles
-extern "C" int dgn_diag_emit_phases(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dgn::dgn_emit_phase), 8 * sizeof(unsigned long long)) != hipSuccess)
-        return -1;
-    if (reset) {
-        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(dgn::dgn_emit_phase), z, sizeof(z)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-#endif

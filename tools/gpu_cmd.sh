@@ -1,7 +1,9 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
-tail -1 gpurun_out/smoke.log
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_betti_wide.py tests/test_gpu_fused.py tests/test_gpu_graph.py > gpurun_out/t_last.log 2>&1 || { tail -30 gpurun_out/t_last.log; exit 1; }
-tail -1 gpurun_out/t_last.log
+mkdir -p gpurun_out/g8
+export TMPDIR=/tmp
+bash tools/pmc_betti.sh gpurun_out/g8/pmc fcc 4 1024 5.0 1 || exit 1
+python3 tools/pmc_summary.py gpurun_out/g8/pmc betti > gpurun_out/g8/pmc.txt
+bash profiles/collect_wide.sh r05base || exit 1
+timeout -k 10 120 python -u tools/side_graph.py 20 > gpurun_out/g8/side_graph.json 2>&1 || exit 1
+echo done
