@@ -8,7 +8,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall 
             -mllvm -amdgpu-atomic-optimizer-strategy=DPP
 LIB      := $(PKG)/lib/libdgn.so
 
-KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/betti_rank.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o
+KOBJS := $(BUILD)/graph_kernels.o $(BUILD)/betti_kernels.o $(BUILD)/betti_wide.o $(BUILD)/betti_rank.o \
+         $(BUILD)/betti_split.o $(BUILD)/node_kernels.o $(BUILD)/dgn_api.o
 
 all: $(LIB) facade oracle
 

@@ -1285,11 +1285,119 @@ int dgn_debug_betti_clouds(dgn_ctx* c, const dgn_batch* h, double rc, int64_t fi
     return DGN_OK;
 }
 
+// Complexes above the kernels' kWideMaxPoints-point envelope (betti_split.hip): split into the
+// connected components of their threshold graph, whose persistence pairs union to the complex's
+// (ripser.cpp:386-395, 514-1269 on a block-diagonal coboundary matrix); each component of two or
+// more points is reduced by the ordinary Betti pass as a caller-given triangle, a one-point
+// component adds one essential dim-0 class. pairs [C][3][cap][2] (unsorted here) and kk [C][4] are
+// filled on the host. A component above kWideMaxPoints points: DGN_ERR_UNSUPPORTED.
+static int persistence_split(dgn_ctx* c, const double* d_clouds, const float* d_lower, const int32_t* d_np,
+                             const int32_t* npoints, int64_t C, int32_t max_points, double threshold, float* pairs,
+                             int32_t cap, std::vector<int32_t>& kk) {
+    const int64_t tri_in = (int64_t)max_points * (max_points - 1) / 2;  // caller-given packing
+    const int64_t tri_stride = (tri_in + 3) / 4 * 4;
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(C, (int64_t(8) << 30) / (4 * tri_stride)));
+    DevBuf tri, lab, dmap, doff, dsize, dsrc, sub, snp, spairs, scnt;
+    if (d_clouds) HIP_TRY(c, tri.ensure(4 * (size_t)(chunk * tri_stride)));
+    HIP_TRY(c, lab.ensure(4 * (size_t)(chunk * max_points)));
+    std::vector<int32_t> labels((size_t)(chunk * max_points));
+    std::fill(kk.begin(), kk.end(), 0);
+    for (int64_t c0 = 0; c0 < C; c0 += chunk) {
+        const int64_t cnt = std::min<int64_t>(chunk, C - c0);
+        const float* T = d_lower ? d_lower + c0 * tri_in : tri.as<float>();
+        const int64_t ts = d_lower ? tri_in : tri_stride;
+        if (d_clouds) HIP_TRY(c, launch_big_gram(c->stream, d_clouds, max_points, d_np, c0, cnt, tri.as<float>(), tri_stride));
+        HIP_TRY(c, launch_components(c->stream, T, ts, d_np, c0, cnt, (float)threshold, lab.as<int32_t>(), max_points));
+        HIP_TRY(c, hipMemcpyAsync(labels.data(), lab.p, 4 * (size_t)(cnt * max_points), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, stream_sync(c));
+        // components (a root is its component's smallest vertex): vertex lists in ascending order
+        std::vector<int32_t> map, src, size;
+        std::vector<int64_t> off;
+        int32_t smax = 1;
+        for (int64_t i = 0; i < cnt; ++i) {
+            const int32_t n = npoints[c0 + i];
+            const int32_t* L = labels.data() + i * max_points;
+            std::vector<int32_t> count((size_t)n, 0);
+            for (int32_t v = 0; v < n; ++v) ++count[(size_t)L[v]];
+            std::vector<int64_t> first((size_t)n, -1);
+            for (int32_t r = 0; r < n; ++r) {
+                if (count[(size_t)r] == 0) continue;
+                if (count[(size_t)r] == 1) {
+                    ++kk[4 * (size_t)(c0 + i) + 1];  // one point: an essential dim-0 class, no pairs
+                    continue;
+                }
+                if (count[(size_t)r] > kWideMaxPoints)
+                    return fail(c, DGN_ERR_UNSUPPORTED,
+                                "a connected component of " + std::to_string(count[(size_t)r]) +
+                                    " points at this threshold exceeds the " + std::to_string(kWideMaxPoints) +
+                                    "-point kernel envelope (see DESIGN.md)");
+                first[(size_t)r] = (int64_t)map.size();
+                off.push_back((int64_t)map.size());
+                size.push_back(count[(size_t)r]);
+                src.push_back((int32_t)i);
+                smax = std::max(smax, count[(size_t)r]);
+                map.resize(map.size() + (size_t)count[(size_t)r]);
+            }
+            std::vector<int32_t> fill((size_t)n, 0);
+            for (int32_t v = 0; v < n; ++v) {
+                const int32_t r = L[v];
+                if (first[(size_t)r] >= 0) map[(size_t)(first[(size_t)r] + fill[(size_t)r]++)] = v;
+            }
+        }
+        const int64_t nsub = (int64_t)size.size();
+        if (nsub == 0) continue;
+        const int64_t sub_stride = (int64_t)smax * (smax - 1) / 2;
+        hipError_t e;
+        if ((e = dmap.ensure(4 * map.size())) || (e = doff.ensure(8 * off.size())) || (e = dsize.ensure(4 * size.size())) ||
+            (e = dsrc.ensure(4 * src.size())) || (e = sub.ensure(4 * (size_t)std::max<int64_t>(nsub * sub_stride, 1))) ||
+            (e = snp.ensure(4 * (size_t)nsub)) || (e = spairs.ensure(8 * 3 * (size_t)nsub * cap)) ||
+            (e = scnt.ensure(16 * (size_t)nsub)))
+            return hip_fail(c, e, "dgn_host_persistence: component split allocation");
+        HIP_TRY(c, hipMemcpyAsync(dmap.p, map.data(), 4 * map.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(doff.p, off.data(), 8 * off.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(dsize.p, size.data(), 4 * size.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(dsrc.p, src.data(), 4 * src.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(snp.p, size.data(), 4 * size.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, launch_gather_sub(c->stream, T, ts, dsrc.as<int32_t>(), doff.as<int64_t>(), dsize.as<int32_t>(),
+                                     dmap.as<int32_t>(), nsub, sub.as<float>(), sub_stride));
+        int st = betti_impl(c, nullptr, threshold, nullptr, scnt.as<int32_t>(), nullptr, snp.as<int32_t>(), smax, nsub,
+                            spairs.as<float>(), cap, sub.as<float>());
+        if (st) return st;
+        std::vector<int32_t> sk(4 * (size_t)nsub);
+        std::vector<float> sp(2 * 3 * (size_t)nsub * cap);
+        HIP_TRY(c, hipMemcpy(sk.data(), scnt.p, 16 * (size_t)nsub, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(sp.data(), spairs.p, 8 * 3 * (size_t)nsub * cap, hipMemcpyDeviceToHost));
+        // the union of the components' pairs (counts past cap are reported by the caller)
+        for (int64_t q = 0; q < nsub; ++q) {
+            const int64_t i = c0 + src[(size_t)q];
+            int32_t* k = kk.data() + 4 * i;
+            k[1] += sk[4 * (size_t)q + 1];
+            const int col[3] = {0, 2, 3};
+            for (int d = 0; d < 3; ++d) {
+                const int32_t m = sk[4 * (size_t)q + col[d]];
+                for (int32_t t = 0; t < m && t < cap; ++t) {
+                    const int32_t slot = k[col[d]] + t;
+                    if (slot >= cap) break;
+                    const float* from = sp.data() + ((size_t)(q * 3 + d) * cap + t) * 2;
+                    float* to = pairs + ((size_t)(i * 3 + d) * cap + slot) * 2;
+                    to[0] = from[0];
+                    to[1] = from[1];
+                }
+                k[col[d]] += m;
+            }
+        }
+    }
+    return DGN_OK;
+}
+
 static int host_persistence_common(dgn_ctx* c, const double* clouds, const float* lower, const int32_t* npoints,
                                    int64_t C, int32_t max_points, double threshold, float* pairs, int32_t cap,
                                    int32_t* counts) {
     if (!c || (!clouds && !lower) || !npoints || C < 0 || max_points <= 0 || cap <= 0 || !pairs)
         return fail(c, DGN_ERR_ARG, "dgn_host_persistence: bad args");
+    if (max_points > kSplitMaxPoints)
+        return fail(c, DGN_ERR_UNSUPPORTED, "dgn_host_persistence: clouds above " + std::to_string(kSplitMaxPoints) +
+                                                " points");
     if (C == 0) return DGN_OK;
     for (int64_t i = 0; i < C; ++i)
         if (npoints[i] < 1 || npoints[i] > max_points) return fail(c, DGN_ERR_ARG, "npoints out of range");
@@ -1303,12 +1411,17 @@ static int host_persistence_common(dgn_ctx* c, const double* clouds, const float
         return hip_fail(c, e, "dgn_host_persistence: allocation");
     HIP_TRY(c, hipMemcpy(dc.p, clouds ? (const void*)clouds : (const void*)lower, in_bytes, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(dn.p, npoints, 4 * (size_t)C, hipMemcpyHostToDevice));
-    int st = betti_impl(c, nullptr, threshold, nullptr, dk.as<int32_t>(), clouds ? dc.as<double>() : nullptr,
-                        dn.as<int32_t>(), max_points, C, dp.as<float>(), cap, clouds ? nullptr : dc.as<float>());
     std::vector<int32_t> kk(4 * C);
+    const bool split = max_points > kWideMaxPoints;  // complexes above the kernels' envelope
+    int st = split ? persistence_split(c, clouds ? dc.as<double>() : nullptr, clouds ? nullptr : dc.as<float>(),
+                                       dn.as<int32_t>(), npoints, C, max_points, threshold, pairs, cap, kk)
+                   : betti_impl(c, nullptr, threshold, nullptr, dk.as<int32_t>(), clouds ? dc.as<double>() : nullptr,
+                                dn.as<int32_t>(), max_points, C, dp.as<float>(), cap, clouds ? nullptr : dc.as<float>());
     if (!st) {
-        HIP_TRY(c, hipMemcpy(kk.data(), dk.p, 16 * (size_t)C, hipMemcpyDeviceToHost));
-        HIP_TRY(c, hipMemcpy(pairs, dp.p, 8 * 3 * (size_t)C * cap, hipMemcpyDeviceToHost));
+        if (!split) {
+            HIP_TRY(c, hipMemcpy(kk.data(), dk.p, 16 * (size_t)C, hipMemcpyDeviceToHost));
+            HIP_TRY(c, hipMemcpy(pairs, dp.p, 8 * 3 * (size_t)C * cap, hipMemcpyDeviceToHost));
+        }
         // sort each diagram ascending by (birth, death) for a canonical order
         for (int64_t i = 0; i < C; ++i) {
             const int n_per[3] = {kk[4 * i], kk[4 * i + 2], kk[4 * i + 3]};

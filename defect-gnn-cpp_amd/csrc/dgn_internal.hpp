@@ -154,6 +154,10 @@ struct BettiLaunch {
 // kWideBigPoints, 11-bit vertices and the adjacency in scratch above) in the retry launch after
 // betti_rank_codes
 constexpr int kWideMaxPoints = 2048;
+// dgn_host_persistence[_lower] above kWideMaxPoints points: split into the connected components of
+// the threshold graph (betti_split.hip), each reduced by the ordinary tiers; the union-find keeps
+// a complex's parents in LDS (4 B per point)
+constexpr int kSplitMaxPoints = 16384;
 constexpr int kWideBigPoints = 1024;
 constexpr int kWideRegular = 512;
 constexpr int kC16MaxPoints = 362;  // C(362, 2) < 2^16: u16 rank codes (wide launch)
@@ -188,6 +192,17 @@ hipError_t betti_rank_codes(hipStream_t s, const float* lower, int64_t tri_strid
 // per slice q < nsl of a list of *total entries (device): sl[2q] = min(slice, max(0, *total - q slice)),
 // sl[2q + 1] = 0 (the slice launch's queue)
 hipError_t launch_slice_lengths(hipStream_t s, const uint32_t* total, int64_t slice, int64_t nsl, uint32_t* sl);
+
+// component split (betti_split.hip): f32 packed triangles of clouds [first, first + count) (VALU
+// Gram, the reference's arithmetic), union-find roots labels[c][v] over d <= thr, and the packed
+// sub-triangle of each listed component (map: ascending vertices at off[q], size[q], of complex src[q])
+hipError_t launch_big_gram(hipStream_t s, const double* clouds, int64_t cloud_stride, const int32_t* npoints,
+                           int64_t first, int64_t count, float* lower, int64_t tri_stride);
+hipError_t launch_components(hipStream_t s, const float* lower, int64_t tri_stride, const int32_t* npoints,
+                             int64_t first, int64_t count, float thr, int32_t* labels, int64_t label_stride);
+hipError_t launch_gather_sub(hipStream_t s, const float* lower, int64_t tri_stride, const int32_t* src,
+                             const int64_t* off, const int32_t* size, const int32_t* map, int64_t count,
+                             float* sub, int64_t sub_stride);
 
 // distance pass over complexes [first, first + count) of a BettiLaunch's cloud input
 struct DistLaunch {

@@ -3,7 +3,9 @@ has no workspace caps (third_party/ripser/ripser.cpp:514-1269): complexes whose 
 a kernel's per-wave workspace (cliques: every pairwise distance <= threshold) must be reduced again
 by the capacity-retry launch (betti_wide_kernel, big layout) instead of failing; a complex that
 outgrows the big layout's tables is listed again and reduced with 4x the tables, up to 2^30
-entries (betti_wide_layout grow levels). Complexes of up to 2,048 points (the HUGE instantiation).
+entries (betti_wide_layout grow levels). Complexes of up to 2,048 points (the HUGE instantiation);
+larger clouds given to dgn_host_persistence are reduced per connected component of their threshold
+graph (each component of up to 2,048 points).
 Counts and (birth, death) pairs bit-exact, compared as sorted multisets."""
 import os
 
@@ -275,14 +277,59 @@ def test_fcc256_cutoff_16A_search_triangles(ctx):
         assert np.array_equal(got.view(np.uint32), mapped.view(np.uint32)), a
 
 
+def _clustered(rng, n, k, spread, big=0):
+    """n points in k Gaussian clusters (plus, if big > 0, one cluster of `big` points) in a 60 A box."""
+    centers = rng.uniform(0, 60, (k, 3))
+    lab = rng.integers(0, k, n - big)
+    pts = centers[lab] + rng.normal(0, spread, (n - big, 3))
+    if big:
+        pts = np.vstack([pts, rng.uniform(0, 60, 3) + rng.normal(0, 2.2, (big, 3))])
+    return pts
+
+
+def test_above_2048_points_split_into_components(ctx):
+    """Clouds of 2,100..3,000 points (dgn_host_persistence / _lower: compute_persistence and
+    compute_persistence_from_distances, ripser_wrapper.cpp:11-70), reduced per connected component of
+    the threshold graph (betti_split.hip; the pairs of a disjoint union are the union of the pairs):
+    clusters of ~20..200 points and isolated points, one 600-point cluster (the rank-coded BIG tier),
+    against verbatim Ripser on the whole cloud."""
+    rng = np.random.default_rng(7)
+    specs = [(2100, 30, 0), (2600, 20, 600), (3000, 60, 0)]
+    npts = np.array([n for n, _, _ in specs], np.int32)
+    clouds = np.zeros((len(specs), npts.max(), 3))
+    for c, (n, k, big) in enumerate(specs):
+        clouds[c, :n] = _clustered(rng, n, k, 1.2, big)
+    thr = 1.6
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=4096)
+    lows = []
+    for c, n in enumerate(npts):
+        low = O.local_distances(clouds[c, :n])
+        lows.append(low)
+        r = O.ref_persistence(low, int(n), np.float32(thr))
+        assert counts[c, 1] == r["n_inf0"], c
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+    # the caller-given distance matrices (the same packed triangles)
+    m = int(npts.max())
+    L = np.zeros((len(specs), m * (m - 1) // 2), np.float32)
+    for c, low in enumerate(lows):
+        L[c, :low.shape[0]] = low
+    pl, cl = ctx.host_persistence_lower(L, npts, m, thr, cap=4096)
+    assert np.array_equal(cl, counts)
+    for c in range(len(specs)):
+        for di, col in enumerate((0, 2, 3)):
+            assert np.array_equal(pl[c, di, :cl[c, col]], pairs[c, di, :counts[c, col]])
+
+
 def test_above_2048_points_fails_loudly(ctx):
     # outside the envelope (DESIGN.md §8): an explicit DGN_ERR_UNSUPPORTED, never a silent or
-    # truncated result -- a caller-given 2,100-point cloud, and FCC-256 at 21 A (~3,100-point
-    # local complexes, the count pass finds them before any Betti launch)
+    # truncated result -- a caller-given 2,100-point cloud whose threshold graph is one connected
+    # component (every point within the threshold of its neighbours), and FCC-256 at 21 A
+    # (~3,100-point local complexes, the count pass finds them before any Betti launch)
     rng = np.random.default_rng(5)
-    cloud = rng.uniform(0.0, 100.0, size=(1, 2100, 3))
+    cloud = rng.uniform(0.0, 12.0, size=(1, 2100, 3))
     with pytest.raises(dgn.DgnError) as e:
-        ctx.host_persistence(cloud, np.array([2100], np.int32), 1.0)
+        ctx.host_persistence(cloud, np.array([2100], np.int32), 3.0)
     assert e.value.status == 5
     with pytest.raises(dgn.DgnError) as e:
         ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 21.0)

@@ -4,7 +4,7 @@
 # Only the listed sources (default: all) are rebuilt with the flags; the rest are the main build's objects.
 set -eo pipefail
 TAG=$1; FLAGS=${2:-}; shift 2 || true
-SRCS=${@:-graph_kernels betti_kernels betti_wide betti_rank node_kernels dgn_api}
+SRCS=${@:-graph_kernels betti_kernels betti_wide betti_rank betti_split node_kernels dgn_api}
 cd "$(dirname "$0")/.."
 make -s defect-gnn-cpp_amd/lib/libdgn.so
 B=defect-gnn-cpp_amd/build_var_$TAG
