@@ -73,23 +73,43 @@ int main(int argc_in, char** argv_in) {
             std::vector<crystal::Structure> st;
             std::vector<size_t> todo;  // ids[i] to compute in this batch
             std::vector<dgn::MatrixXd> feats(hi - lo);
+            std::vector<crystal::Structure> parsed;
+            parsed.reserve(hi - lo);
+            for (size_t i = lo; i < hi; ++i) parsed.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
             for (size_t i = lo; i < hi; ++i) {
                 const std::string out = processed_path + "/betti/" + ids[i] + ".bin";
+                bool have = false;
                 if (resume && fs::exists(out)) {
-                    feats[i - lo] = topology::load_betti_features(out);
-                    ++skipped;
-                } else {
-                    todo.push_back(i);
+                    // an unreadable file (a run killed mid-write before round 5 wrote them in place) or
+                    // one of another shape (other structure) is recomputed, not trusted
+                    try {
+                        dgn::MatrixXd m = topology::load_betti_features(out);
+                        if (m.rows() == static_cast<std::ptrdiff_t>(parsed[i - lo].num_atoms()) &&
+                            m.cols() == topology::BETTI_FEATURE_DIM) {
+                            feats[i - lo] = std::move(m);
+                            have = true;
+                            ++skipped;
+                        } else {
+                            log("resume: " + out + " has the wrong shape; recomputed");
+                        }
+                    } catch (const std::exception& e) {
+                        log(std::string("resume: ") + e.what() + "; recomputed");
+                    }
                 }
+                if (!have) todo.push_back(i);
             }
             st.reserve(todo.size());
-            for (size_t i : todo) st.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
+            for (size_t i : todo) st.push_back(parsed[i - lo]);
             std::vector<const crystal::Structure*> ptrs;
             for (const auto& s : st) ptrs.push_back(&s);
             if (!ptrs.empty()) {
                 std::vector<dgn::MatrixXd> got = topology::compute_batch_betti_features(ptrs, r_cutoff);
                 for (size_t t = 0; t < todo.size(); ++t) {
-                    topology::save_betti_features(processed_path + "/betti/" + ids[todo[t]] + ".bin", got[t]);
+                    // written under a temporary name and renamed into place: a killed run never
+                    // leaves a truncated betti/<id>.bin behind for --resume
+                    const std::string out = processed_path + "/betti/" + ids[todo[t]] + ".bin";
+                    topology::save_betti_features(out + ".tmp", got[t]);
+                    fs::rename(out + ".tmp", out);
                     feats[todo[t] - lo] = std::move(got[t]);
                 }
             }

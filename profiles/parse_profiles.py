@@ -56,7 +56,7 @@ def main():
         with open(trace) as f:
             for r in csv.DictReader(f):
                 name = r["Kernel_Name"]
-                for k in PATH_KERNELS + ("betti_dist_search_kernel", "betti_kernel<44>", "betti_kernel<48>"):
+                for k in PATH_KERNELS + ("betti_dist_search_kernel", "betti_kernel<44>", "betti_kernel<48>", "betti_kernel<64>"):
                     if k in name:
                         ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
                         launches.setdefault(k, []).append(round(ms, 4))

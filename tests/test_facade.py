@@ -218,3 +218,24 @@ def test_preprocess_driver_resume(tmp_path, golden):
         if b != victim:
             assert os.stat(b).st_mtime_ns == first[b][1], b  # not rewritten
     assert open(outdir / "pca_model.bin", "rb").read() == pca1
+
+
+@pytest.mark.gpu
+def test_preprocess_driver_resume_recomputes_bad_files(tmp_path, golden):
+    """--resume never trusts a betti/<id>.bin it cannot use: a truncated file (a run killed
+    mid-write) and one with another structure's row count are recomputed (byte-identical to a
+    fresh run) instead of aborting the run or feeding the PCA; no .tmp file is left behind."""
+    outdir = tmp_path / "processed"
+    exe = os.path.join(BIN, "preprocess_betti")
+    rc, _, err = _run([exe, POSCARS, str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    good = {b: open(b, "rb").read() for b in glob.glob(str(outdir / "betti" / "*.bin"))}
+    trunc, other = str(outdir / "betti" / "741.bin"), str(outdir / "betti" / "1.bin")
+    open(trunc, "wb").write(good[trunc][:100])
+    open(other, "wb").write(good[str(outdir / "betti" / "1046.bin")])
+    rc, _, err = _run([exe, "--resume", POSCARS, str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    assert "resume: 7 existing" in err
+    for b, data in good.items():
+        assert open(b, "rb").read() == data, b
+    assert not glob.glob(str(outdir / "betti" / "*.tmp"))
