@@ -127,8 +127,9 @@ def main():
     wide = {}
     for sub in ("wide_fetch", "wide_write", "wide_sq1", "wide_sq2"):
         for r in rows(sub):
-            if "betti_wide" in r["Kernel_Name"]:
-                wide[r["Counter_Name"]] = float(r["Counter_Value"])
+            # the u16-code wide launch (the device-driven retry launch beside it is empty here)
+            if "betti_wide_kernel_c16" in r["Kernel_Name"]:
+                wide[r["Counter_Name"]] = wide.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     st = {}
     p = glob.glob(os.path.join(D, "wide_trace", "**", "*kernel_stats.csv"), recursive=True)
     if p:

@@ -1,9 +1,7 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out/g8
+mkdir -p gpurun_out/g10
 export TMPDIR=/tmp
-bash tools/pmc_betti.sh gpurun_out/g8/pmc fcc 4 1024 5.0 1 || exit 1
-python3 tools/pmc_summary.py gpurun_out/g8/pmc betti > gpurun_out/g8/pmc.txt
-bash profiles/collect_wide.sh r05base || exit 1
-timeout -k 10 120 python -u tools/side_graph.py 20 > gpurun_out/g8/side_graph.json 2>&1 || exit 1
-echo done
+timeout -k 10 600 python -u bench.py > gpurun_out/g10/bench.json 2> gpurun_out/g10/bench.err || { tail -20 gpurun_out/g10/bench.err; exit 1; }
+tail -c 3000 gpurun_out/g10/bench.json
+timeout -k 10 1200 bash profiles/collect_r05.sh gpurun_out/prof_r05a
