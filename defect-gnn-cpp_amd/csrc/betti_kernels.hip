@@ -1269,7 +1269,8 @@ __global__ __launch_bounds__(kWave, betti_waves_per_simd<NP>()) void betti_kerne
 
 // ---------------------------------------------------------------------------------------
 // Local distance matrices of caller-given clouds (dgn_host_persistence: compute_persistence,
-// ripser_wrapper.cpp:60-70) on the matrix cores (gram_triangle_*, dgn_device.hpp). One wave per
+// ripser_wrapper.cpp:60-70): gram_triangle_* (dgn_device.hpp; VALU pairs up to 64 points, matrix-
+// core Gram tiles above). One wave per
 // complex. The atom-centred clouds of dgn_*_betti come from betti_dist_search_kernel
 // (graph_kernels.hip), which finds the neighbours itself.
 // ---------------------------------------------------------------------------------------

@@ -392,8 +392,9 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
     double* key_rows = nullptr;
     if (cap == kEmitGlobalKeys) {
         // rows of more candidates than the LDS holds (neighbor_list.cpp:27-66 has no cap): per-wave
-        // key rows in HBM for one chunk of tiles (~0.4 GB at 2,700 candidates), kept for reuse
-        HIP_TRY(c, c->emit_keys.ensure((size_t)emit_key_rows_per_chunk() * (size_t)emit_key_row_doubles(W.max_candidates) *
+        // key rows in HBM for one chunk of tiles (<= kEmitGkChunkBytes), kept for reuse
+        HIP_TRY(c, c->emit_keys.ensure((size_t)emit_key_rows_per_chunk(W.max_candidates) *
+                                       (size_t)emit_key_row_doubles(W.max_candidates) *
                                        sizeof(double)));
         key_rows = c->emit_keys.as<double>();
     }

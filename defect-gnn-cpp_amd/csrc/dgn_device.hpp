@@ -102,7 +102,17 @@ __device__ __forceinline__ T wave_inclusive_sum(T v) {
 // result), row_bcast:15 / row_bcast:31 carry rows 0..2 into row 3, and one v_readlane of lane 63.
 // The result is uniform to the compiler; a __shfl-based reduction is a vector value to it, and a
 // branch on one turns every later branch on data derived from it into exec-masked code.
+// Precondition: the whole wave is active (EXEC = all 64 lanes), i.e. the call sits in wave-uniform
+// control flow. An inactive lane would be read by the DPP steps as the bound value (the identity,
+// harmless), but an inactive lane 63 would hand back a stale register. Builds with
+// -DDGN_DEVICE_CHECKS=1 trap on a call that breaks the precondition.
+__device__ __forceinline__ void dgn_check_full_exec() {
+#if defined(DGN_DEVICE_CHECKS) && DGN_DEVICE_CHECKS
+    if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
+#endif
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    dgn_check_full_exec();
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xf, 0xf, false));
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x122, 0xf, 0xf, false));
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x124, 0xf, 0xf, false));
@@ -120,6 +130,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return ((uint64_t)mh << 32) | ml;
 }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+    dgn_check_full_exec();
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xf, 0xf, false);
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xf, 0xf, false);
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xf, 0xf, false);
@@ -137,46 +148,65 @@ __device__ __forceinline__ void wave_lds_sync() { __builtin_amdgcn_fence(__ATOMI
 
 __device__ __forceinline__ int tri_c2(int x) { return x * (x - 1) / 2; }
 
-// ---- local distance matrix on the matrix cores (ripser_wrapper.cpp:60-70 + 17-24) ----
-// The K = 3 Gram product as three rank-1 v_mfma_f64_16x16x4_f64 per 16 x 16 tile (operand k'
-// nonzero only for k' == k, so each product is exactly round(x_ik * x_jk)), summed (p0 + p1) + p2
-// on the VALU, then sqrt(max(0, (sq_i + sq_j) - 2 dot)) -> f32: bit-identical to the reference's
-// Eigen path. Writes the strict lower triangle in the reference's packing (row i, j < i at
-// i(i-1)/2 + j). Narrow form: n <= 64, lane p holds cloud row p in px (lanes >= n: any value);
-// sq = per-wave LDS [64].
-__device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, double* sq, float* __restrict__ L) {
-    typedef double double4_t __attribute__((ext_vector_type(4)));
+// ---- local distance matrices (ripser_wrapper.cpp:60-70 + 17-24) ----
+// The reference's Gram arithmetic: dot = (x_i0 x_j0 + x_i1 x_j1) + x_i2 x_j2 (Eigen's GEBP k
+// order, each product rounded, no FMA), sq_i = the same sum of squares, then
+// sqrt(max(0, (sq_i + sq_j) - 2 dot)) -> f32; the strict lower triangle in the reference's packing
+// (row i, j < i at i(i-1)/2 + j).
+//
+// sqrt_lean: the f64 square root the compiler emits for sqrt() (v_rsq_f64 seed, one Newton step
+// on the pair (y ~ sqrt x, h ~ 1/(2 sqrt x)), two residual corrections), without its rescaling of
+// x < 2^-767 and its +-0 / inf pass-through: the same operations in the same order, so for
+// 2^-767 <= x < inf it returns the same bits. The callers take the full sqrt() for a wave with
+// any lane outside that range.
+__device__ __forceinline__ double sqrt_lean(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double y = x * r;
+    double h = r * 0.5;
+    const double e = __builtin_fma(-h, y, 0.5);
+    y = __builtin_fma(y, e, y);
+    h = __builtin_fma(h, e, h);
+    double d = __builtin_fma(-y, y, x);
+    y = __builtin_fma(d, h, y);
+    d = __builtin_fma(-y, y, x);
+    return __builtin_fma(d, h, y);
+}
+constexpr double kLeanSqrtMin = 0x1p-767;  // the compiler's rescaling threshold
+
+// Narrow form: n <= 64, lane p holds cloud row p in px (lanes >= n: any value); rec = per-wave
+// LDS [4 * 64] doubles (x, y, z, squared norm per row; it may overlay the storage px came from).
+// One pair per lane and round over the packed triangle, so every lane of a round but the last
+// computes a wanted distance and the stores are contiguous (a 16 x 16 Gram tile on the matrix
+// cores leaves 37 % of the lanes idle at n = 43 and its products need the same VALU tail: the
+// MFMA form measured 4.55 ms of the 5.94 ms config-4 distance kernel, the search 1.39 ms).
+__device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, double* rec, float* __restrict__ L) {
+    typedef double double2_t __attribute__((ext_vector_type(2)));
     const int lane = lane_id();
-    sq[lane] = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
-    const int T = (n + 15) / 16;
-    const int kk = lane >> 4;
-    double xr[4];  // coordinate kk of cloud row 16 I + (lane & 15)
-#pragma unroll
-    for (int I = 0; I < 4; ++I) {
-        const int ra = 16 * I + (lane & 15);
-        const double v0 = __shfl(px[0], ra, kWave), v1 = __shfl(px[1], ra, kWave), v2 = __shfl(px[2], ra, kWave);
-        xr[I] = (ra < n && kk < 3) ? (kk == 0 ? v0 : (kk == 1 ? v1 : v2)) : 0.0;
+    const double sq = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
+    wave_lds_sync();
+    if (lane < n) {
+        double2_t* R = reinterpret_cast<double2_t*>(rec + 4 * lane);
+        R[0] = double2_t{px[0], px[1]};
+        R[1] = double2_t{px[2], sq};
     }
     wave_lds_sync();
-    for (int I = 0; I < T; ++I) {
-        for (int J = 0; J <= I; ++J) {
-            const double xa = I == 0 ? xr[0] : (I == 1 ? xr[1] : (I == 2 ? xr[2] : xr[3]));
-            const double xb = J == 0 ? xr[0] : (J == 1 ? xr[1] : (J == 2 ? xr[2] : xr[3]));
-            const double4_t z = {0.0, 0.0, 0.0, 0.0};
-            const double4_t p0 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 0 ? xa : 0.0, kk == 0 ? xb : 0.0, z, 0, 0, 0);
-            const double4_t p1 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 1 ? xa : 0.0, kk == 1 ? xb : 0.0, z, 0, 0, 0);
-            const double4_t p2 = __builtin_amdgcn_mfma_f64_16x16x4f64(kk == 2 ? xa : 0.0, kk == 2 ? xb : 0.0, z, 0, 0, 0);
-            const int col = 16 * J + (lane & 15);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = 16 * I + (lane >> 4) + 4 * r;
-                if (row < n && col < row) {  // strict lower triangle (ripser_wrapper.cpp:20-24)
-                    const double dot = (p0[r] + p1[r]) + p2[r];  // GEBP k order, no FMA
-                    const double d2 = (sq[row] + sq[col]) - 2.0 * dot;
-                    L[tri_c2(row) + col] = (float)sqrt(fmax(d2, 0.0));
-                }
-            }
-        }
+    const int tot = tri_c2(n);
+    for (int t = lane; t - lane < tot; t += kWave) {
+        if (t >= tot) break;
+        // row i of packed index t (t < 2016): the f32 root of 8t + 1 is within one of the answer
+        int i = (int)((1.0f + __builtin_amdgcn_sqrtf((float)(8 * t + 1))) * 0.5f);
+        i -= tri_c2(i) > t;
+        i += tri_c2(i + 1) <= t;
+        const int j = t - tri_c2(i);
+        const double2_t* Ri = reinterpret_cast<const double2_t*>(rec + 4 * i);
+        const double2_t* Rj = reinterpret_cast<const double2_t*>(rec + 4 * j);
+        const double2_t a0 = Ri[0], a1 = Ri[1], b0 = Rj[0], b1 = Rj[1];
+        const double dot = (a0.x * b0.x + a0.y * b0.y) + a1.x * b1.x;  // GEBP k order, no FMA
+        const double d2 = fmax((a1.y + b1.y) - 2.0 * dot, 0.0);
+        double dd;
+        if (ballot(!(d2 >= kLeanSqrtMin && d2 < __builtin_inf()))) dd = sqrt(d2);
+        else dd = sqrt_lean(d2);
+        L[t] = (float)dd;
     }
     wave_lds_sync();
 }

@@ -71,12 +71,14 @@ hipError_t launch_block_scan(hipStream_t s, int64_t* block_sums, const uint64_t*
 // Fused emit: each block re-runs the search for its atoms, ranks, writes row_ptr / col / dist /
 // disp and the RBF. cap = graph_emit_cap(max candidates of the count pass, kmax): 64..2048 (the
 // per-wave hit lists in LDS) or kEmitGlobalKeys (rows of more candidates: key_rows, caller-owned,
-// emit_key_rows_per_chunk() rows of emit_key_row_doubles(max_candidates) doubles); stage = atoms
+// emit_key_rows_per_chunk(max_candidates) rows of emit_key_row_doubles(max_candidates) doubles); stage = atoms
 // staged in LDS (max structure size if <= kStage, else 0).
 constexpr int kEmitGlobalKeys = -1;
-constexpr int64_t kEmitGkChunkBlocks = 2048;  // tiles per launch of the global-key emit
+constexpr int64_t kEmitGkChunkBlocks = 2048;        // tiles per launch of the global-key emit, at most
+constexpr int64_t kEmitGkChunkBytes = 256ll << 20;  // key-row bytes per launch, at most (>= one tile)
 int64_t emit_key_row_doubles(uint32_t max_candidates);
-int64_t emit_key_rows_per_chunk();
+int64_t emit_key_chunk_tiles(uint32_t max_candidates);
+int64_t emit_key_rows_per_chunk(uint32_t max_candidates);
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag,

@@ -1883,7 +1883,8 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 // NeighborList(rc, SIZE_MAX), :107). The persistence diagram and the 35 statistics do not depend
 // on the order of the cloud's rows (every distance depends only on its two points; the pairing
 // values of a filtration do not depend on its tie-breaking order), so the rows keep the search's
-// order instead of the sorted one. Writes the f32 lower triangle (MFMA Gram product) + npoints.
+// order instead of the sorted one. Writes the f32 lower triangle (the reference's Gram arithmetic,
+// gram_triangle_*) + npoints.
 // ------------------------------------------------------------------------------------------
 // The Betti search + MFMA distance kernel writes ~1 KB of triangle per complex with little reuse:
 // compiled for 4 waves per SIMD (128 VGPRs, a few spills) it keeps more stores in flight than at
@@ -1904,12 +1905,15 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
                                                                          int key_stride) {
     __shared__ double stage_mem[kStage * kStageBytesPerAtom / 8];
     DGN_SEARCH_SMEM
-    __shared__ uint64_t key_j[kW][CAP];
-    __shared__ double sq_s[kW][CAP + 1 > kWave ? CAP + 1 : kWave];
+    // per wave: the neighbour keys (CAP u64), then the wide triangle's squared norms (CAP + 1);
+    // the narrow triangle's point records (4 x 64 doubles) overlay both once the cloud is built
+    constexpr int kWaveDoubles = 2 * CAP + 1 > 4 * kWave ? 2 * CAP + 1 : 4 * kWave;
+    __shared__ double cloud_s[kW][kWaveDoubles];
     __shared__ uint64_t mask_s[kQA][kMaskWords];
     const StageView st = make_stage(stage_mem, kStage, offt_s);
     const int w = threadIdx.x / kWave;
     const int lane = lane_id();
+    uint64_t* key_j = reinterpret_cast<uint64_t*>(cloud_s[w]);
     const int64_t g0 = first + (int64_t)blockIdx.x * kQA;
     const int nq = (int)(first + count - g0 < kQA ? first + count - g0 : kQA);
     if (g.mask) {
@@ -1940,7 +1944,7 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
                     bool inr;
                     const double d2 = exact_one(M, P.st, P.st.fx[li], P.st.fx[j], j, q, n, inr);
                     ok = inr && d2 < g.rc2;
-                    key_j[w][lane] = pack_jimg(j, n[0], n[1], n[2]);
+                    key_j[lane] = pack_jimg(j, n[0], n[1], n[2]);
                 }
                 if (ballot(!ok)) {
                     if (lane == 0) atomicOr(error_flag, kGErrMismatch);
@@ -1953,7 +1957,7 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
                 const uint64_t bal = ballot(hit);
                 if (hit) {
                     const int slot = m + mask_prefix(bal);
-                    if (slot < CAP) key_j[w][slot] = pack_jimg(j, na, nb, nc);
+                    if (slot < CAP) key_j[slot] = pack_jimg(j, na, nb, nc);
                 }
                 m += __popcll(bal);
             });
@@ -1965,7 +1969,7 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
         }
         wave_lds_sync();
         if (keys_out)  // diagnostics (dgn_debug_betti_clouds): cloud row p >= 1 is (j, image) key p - 1
-            for (int p = lane; p < m && p < key_stride; p += kWave) keys_out[c * key_stride + p] = key_j[w][p];
+            for (int p = lane; p < m && p < key_stride; p += kWave) keys_out[c * key_stride + p] = key_j[p];
         // cloud row p: p = 0 the centre, else centre + ((p_j + offset) - centre)
         auto point = [&](int p, double x[3]) __attribute__((always_inline)) {
             if (p == 0) {
@@ -1975,7 +1979,7 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
                 return;
             }
             int j, na, nb, nc;
-            unpack_jimg(key_j[w][p - 1], j, na, nb, nc);
+            unpack_jimg(key_j[p - 1], j, na, nb, nc);
             double pj[3];
             P.get(j, pj);
 #pragma unroll
@@ -1988,9 +1992,9 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
         if (n <= kWave) {
             double px[3];
             point(lane < n ? lane : n - 1, px);
-            gram_triangle_narrow(px, n, sq_s[w], L);
+            gram_triangle_narrow(px, n, cloud_s[w], L);
         } else {
-            gram_triangle_wide(n, sq_s[w], L, point);
+            gram_triangle_wide(n, cloud_s[w] + CAP, L, point);
         }
     });
 }
@@ -2100,7 +2104,12 @@ int graph_emit_cap(uint32_t m, uint64_t kmax) {
 }
 
 int64_t emit_key_row_doubles(uint32_t m) { return 3 * (int64_t)((m + 63) / 64 * 64) + 1; }
-int64_t emit_key_rows_per_chunk() { return kEmitGkChunkBlocks * kW; }
+// a chunk's key rows take at most kEmitGkChunkBytes whatever max_candidates is (at least one tile)
+int64_t emit_key_chunk_tiles(uint32_t m) {
+    const int64_t tile_bytes = emit_key_row_doubles(m) * (int64_t)sizeof(double) * kW;
+    return std::max<int64_t>(1, std::min<int64_t>(kEmitGkChunkBlocks, kEmitGkChunkBytes / tile_bytes));
+}
+int64_t emit_key_rows_per_chunk(uint32_t m) { return emit_key_chunk_tiles(m) * kW; }
 
 template <int CAP, bool STREAM>
 static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const int32_t* counts,
@@ -2121,9 +2130,9 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
                                rs, error_flag, tl, gk);
     };
     if (CAP == 0) {
-        // global key rows: one row per wave of a chunk of kEmitGkChunkBlocks tiles, launched in turn
-        for (int64_t t0 = 0; t0 < nt; t0 += kEmitGkChunkBlocks)
-            go({t0, std::min<int64_t>(kEmitGkChunkBlocks, nt - t0), 0, 0, fused});
+        // global key rows: one row per wave of a chunk of emit_key_chunk_tiles tiles, launched in turn
+        const int64_t chunk = emit_key_chunk_tiles((uint32_t)gk.cap);
+        for (int64_t t0 = 0; t0 < nt; t0 += chunk) go({t0, std::min<int64_t>(chunk, nt - t0), 0, 0, fused});
         return;
     }
     // one launch, each block writes its rows, then its tile's RBF (round 3 A/B: all rows then all
