@@ -190,14 +190,14 @@ __device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, 
         R[1] = double2_t{px[2], sq};
     }
     wave_lds_sync();
-    const int tot = tri_c2(n);
-    for (int t = lane; t - lane < tot; t += kWave) {
-        if (t >= tot) break;
-        // row i of packed index t (t < 2016): the f32 root of 8t + 1 is within one of the answer
-        int i = (int)((1.0f + __builtin_amdgcn_sqrtf((float)(8 * t + 1))) * 0.5f);
-        i -= tri_c2(i) > t;
-        i += tri_c2(i + 1) <= t;
-        const int j = t - tri_c2(i);
+    const int tot = __builtin_amdgcn_readfirstlane(tri_c2(n));  // n is wave-uniform
+    for (int base = 0; base < tot; base += kWave) {  // wave-uniform rounds; the last one partial
+        const uint32_t t = (uint32_t)min(base + lane, tot - 1);
+        // row i of packed index t < 2016: (1 + sqrt(8t + 1)) / 2 is i exactly at the row's first
+        // index and at most i + 1 - 2 / 127 at its last, so a 0.004 bias absorbs the f32 root's
+        // error (one ulp) without the two integer corrections
+        const uint32_t i = (uint32_t)__builtin_fmaf(__builtin_amdgcn_sqrtf((float)(8 * t + 1)), 0.5f, 0.504f);
+        const uint32_t j = t - ((i * (i - 1)) >> 1);
         const double2_t* Ri = reinterpret_cast<const double2_t*>(rec + 4 * i);
         const double2_t* Rj = reinterpret_cast<const double2_t*>(rec + 4 * j);
         const double2_t a0 = Ri[0], a1 = Ri[1], b0 = Rj[0], b1 = Rj[1];
@@ -206,7 +206,7 @@ __device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, 
         double dd;
         if (ballot(!(d2 >= kLeanSqrtMin && d2 < __builtin_inf()))) dd = sqrt(d2);
         else dd = sqrt_lean(d2);
-        L[t] = (float)dd;
+        if (base + lane < tot) L[t] = (float)dd;
     }
     wave_lds_sync();
 }

@@ -1,7 +1,7 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out/g15
+mkdir -p gpurun_out/g16
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_betti.py tests/test_gpu_betti_cellist.py tests/test_gpu_betti_wide.py tests/test_gpu_betti_envelope.py > gpurun_out/g15/t.log 2>&1 || { tail -30 gpurun_out/g15/t.log; exit 1; }
-tail -3 gpurun_out/g15/t.log
-timeout -k 10 600 bash tools/ab.sh gpurun_out/g15/ab 2 pre base
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_betti.py tests/test_gpu_betti_cellist.py > gpurun_out/g16/t.log 2>&1 || { tail -30 gpurun_out/g16/t.log; exit 1; }
+tail -3 gpurun_out/g16/t.log
+timeout -k 10 600 bash tools/ab.sh gpurun_out/g16/ab 2 pre base
