@@ -3,7 +3,7 @@
 #   bash profiles/collect_r05.sh <outdir>
 # 1. kernel trace + stats of the default bench step (N=1, 8,192 FCC-256, graph + Betti)
 # 2. FETCH_SIZE / WRITE_SIZE passes (separate; gfx950 TCC limits) of the graph-only bench
-# 3. MFMA counters of the distance kernel (betti_dist_search_kernel) inside the bench step
+# 3. SQ counters of the distance kernel (betti_dist_search_kernel: f64 VALU pairs) inside the bench step
 # 4. narrow Betti kernel SQ instruction mix / waits / LDS bank conflicts and TCP/TCC requests
 #    (tools/betti_run.py: 2,048 FCC-256 structures at 5 A)
 # 5. the 10 A wide kernel: FETCH/WRITE and SQ issue/wait (tools/betti_rc10.py, 16 FCC-256)
@@ -19,9 +19,9 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetc
     python3 $BENCH --no-betti --no-alt-rbf > "$OUT/fetch_bench.json" 2> "$OUT/fetch_bench.err"
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 $BENCH --no-betti --no-alt-rbf > "$OUT/write_bench.json" 2> "$OUT/write_bench.err"; echo "2 traffic ok"
-timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU \
-    --kernel-include-regex betti_dist --output-format csv -d "$OUT/mfma" -o run -- \
-    python3 $BENCH > "$OUT/mfma_bench.json" 2> "$OUT/mfma_bench.err"; echo "3 mfma ok"
+timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_LDS \
+    --kernel-include-regex betti_dist --output-format csv -d "$OUT/dist" -o run -- \
+    python3 $BENCH > "$OUT/dist_bench.json" 2> "$OUT/dist_bench.err"; echo "3 dist ok"
 RUN="tools/betti_run.py fcc 4 2048 5.0 1"
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
     --kernel-include-regex betti_kernel --output-format csv -d "$OUT/narrow_sq1" -o run -- python3 $RUN > "$OUT/narrow_sq1.log" 2>&1

@@ -6,7 +6,7 @@ Writes (profiles/):
   r05_narrow_before_after.json             narrow kernels per complex: round 4 (f32 LDS matrix, NP 44 + 48 tiers)
                                            -> u16 rank codes at 6 and 8 waves per SIMD (1,024 FCC-256 at 5 A,
                                            tools/pmc_betti.sh; gpurun_out/g4, g8)
-  r05_mfma.json                            distance kernel MFMA counters + derived rates
+  r05_dist.json                            distance kernel SQ counters (f64 VALU pairs) + derived rates
   r05_rc10_wide.json                       the 10 A wide kernel: time, HBM bytes and SQ mix per complex
   r05_side_graph.json                      per-kernel medians of BASELINE configs 2 and 5 (f32 / f64 RBF)
 SQ cycle counters are in quad-cycles (MI355X_MICROARCH.md); instruction counters per wave instruction.
@@ -20,7 +20,6 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 D = sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(HERE), "gpurun_out", "prof_r05a")
-FP64_MFMA_PEAK_TFS = 78.6
 CLOCK_GHZ = 2.4
 SIMDS = 1024
 
@@ -103,24 +102,20 @@ def main():
                     f.write(f"    {c:32s} {v:18.1f}\n")
     pmc_text("narrow_mem", os.path.join(HERE, "r05_narrow_mem.txt"))
     narrow_before_after()
-    # MFMA counters of the distance kernel (betti_dist_search_kernel<64>), durations from the bench trace
-    m = per_kernel("mfma").get("void dgn::betti_dist_search_kernel<64>", {})
+    # SQ counters of the distance kernel (betti_dist_search_kernel<64>), durations from the bench trace
+    m = per_kernel("dist").get("void dgn::betti_dist_search_kernel<64>", {})
     summ = json.load(open(os.path.join(HERE, "r05_summary.json")))
     dur = summ["trace_launch_ms"]["betti_dist_search_kernel"]
     ms = sum(dur) / len(dur)
-    flops_issued = m["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512  # MfmaFlopsF64 (rocprofiler counter_defs.yaml)
+    nc = 8192 * 256
     mf = {"kernel": "betti_dist_search_kernel<64> (config-4 shard: 2,097,152 local complexes of <= 64 points)",
           "counters_per_launch": m, "avg_launch_ms": round(ms, 4),
-          "mfma_f64_flops_issued_per_launch": flops_issued,
-          "mfma_f64_issued_tflops": round(flops_issued / (ms * 1e-3) / 1e12, 3),
-          "mfma_f64_issued_frac_of_peak": round(flops_issued / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFS, 4),
-          "mfma_busy_frac": round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (ms * 1e-3 * CLOCK_GHZ * 1e9 * SIMDS), 4),
-          "useful": summ["trace_bench"]["roofline_mfma"],
-          "note": "each 16x16 tile issues three v_mfma_f64_16x16x4_f64 with one live k each (exact products, the "
-                  "reference's (p0 + p1) + p2 order), so 1/4 of the issued flops are the K = 3 Gram product and the "
-                  "useful 6n^2 per complex is a smaller figure still (padding to 16-row tiles); MfmaFlopsF64 = "
-                  "SQ_INSTS_VALU_MFMA_MOPS_F64 x 512; busy = SQ_VALU_MFMA_BUSY_CYCLES / (launch cycles x 1,024 SIMDs)"}
-    json.dump(mf, open(os.path.join(HERE, "r05_mfma.json"), "w"), indent=1)
+          "per_complex": {c: round(v / nc, 1) for c, v in m.items()},
+          "issue_frac": round(m["SQ_ACTIVE_INST_ANY"] / m["SQ_WAVE_CYCLES"], 3) if m.get("SQ_WAVE_CYCLES") else None,
+          "useful": summ["trace_bench"].get("roofline_dist"),
+          "note": "one packed pair per lane on the f64 VALU (Gram arithmetic in the reference's order, lean f64 "
+                  "square root); SQ cycle counters in quad-cycles"}
+    json.dump(mf, open(os.path.join(HERE, "r05_dist.json"), "w"), indent=1)
 
     # the 10 A wide kernel (tools/betti_rc10.py 16 1: 4,096 complexes)
     nc = 4096

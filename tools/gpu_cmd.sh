@@ -1,7 +1,6 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out/g16
+mkdir -p gpurun_out/g24
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_betti.py tests/test_gpu_betti_cellist.py > gpurun_out/g16/t.log 2>&1 || { tail -30 gpurun_out/g16/t.log; exit 1; }
-tail -3 gpurun_out/g16/t.log
-timeout -k 10 600 bash tools/ab.sh gpurun_out/g16/ab 2 pre base
+DGN_LIB=defect-gnn-cpp_amd/lib/libdgn_dbg.so timeout -k 10 300 python -u tools/betti_rc10.py 1 1 > gpurun_out/g24/dbg.log 2>&1 || { tail -20 gpurun_out/g24/dbg.log; exit 1; }
+grep DBG gpurun_out/g24/dbg.log | head -20
