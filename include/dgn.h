@@ -262,7 +262,7 @@ int dgn_host_persistence_lower(dgn_ctx* ctx, const float* lower, const int32_t* 
 
 /* Diagnostics (parity tests): the local complexes of atoms [atom_first, atom_first + count) of a
  * host batch as the Betti pass's distance kernel builds them (NeighborList(rc, SIZE_MAX) search +
- * MFMA Gram distances, betti_features.cpp:67-73 / ripser_wrapper.cpp:20-24). lower: [count]
+ * Gram distances, betti_features.cpp:67-73 / ripser_wrapper.cpp:20-24). lower: [count]
  * [max_points*(max_points-1)/2] f32 strict lower triangles in the kernel's cloud row order;
  * npoints[count]; keys (optional): [count][max_points] int64, row p >= 1 of the cloud is neighbour
  * key[p-1] = (j << 24) | (na+128) << 16 | (nb+128) << 8 | (nc+128) (atom j, lattice image
