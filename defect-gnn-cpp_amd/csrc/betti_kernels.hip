@@ -758,24 +758,25 @@ __device__ __forceinline__ void bitonic_sort_regs(uint64_t (&x)[R], int lane) {
 // occurrence among the complex's sorted distances <= thr (order- and equality-preserving),
 // kNoCode above thr (sparse_distance_matrix keeps d <= thr, ripser.cpp:386-395) and on the
 // diagonal -- and sv_out[code] = d (the decode table). The m distances <= thr are compacted
-// (ballots) into scratch as (f32 bits << 12 | i << 6 | j) keys, sorted in registers (bitonic, R
-// per lane: 512 or 1,024 keys), and each sorted key scatters its run's first index to (i, j) and
-// (j, i). Returns the code of 0.0f if the complex has a zero distance, ~0u if it has none, and
+// (ballots) as (f32 bits << 12 | i << 6 | j) keys into the matrix region of the LDS (free until
+// the codes are written), sorted in registers (bitonic, R per lane: 512 or 1,024 keys), and each
+// sorted key scatters its run's first index to (i, j) and (j, i). Returns the code of 0.0f if the complex has a zero distance, ~0u if it has none, and
 // kRankDense if more than kRankMax<NP> distances are <= thr (R = 8 registers per lane in the
 // 32- and 48-point tiers: 512 keys, the dense launch takes the rest; 16 in the 64-point tier:
 // 1,024, the capacity retry takes the rest).
 constexpr uint32_t kRankDense = 0xFFFFFFFEu;
 template <int NP>
 constexpr int kRankMax = NP <= 48 ? 512 : 1024;
-template <int R>
-__device__ __forceinline__ uint32_t rank_sorted(uint16_t* D, int S, const uint64_t* keys, int m, float* sv_out,
+template <int R, class KeyAt, class Clear>
+__device__ __forceinline__ uint32_t rank_sorted(uint16_t* D, int S, KeyAt&& key_at, Clear&& clear, int m, float* sv_out,
                                                 int lane) {
     uint64_t x[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int e = lane * R + r;
-        x[r] = e < m ? at(keys, e) : ~0ull;
+        x[r] = e < m ? key_at(e) : ~0ull;
     }
+    clear();  // the keys are in registers: the matrix region may be overwritten
     bitonic_sort_regs<R>(x, lane);
     // code = the first index of the element's value run = the running maximum of (e if element
     // e starts a run, else 0): within the lane, then across lanes (exclusive max-scan)
@@ -820,16 +821,15 @@ template <int NP>
 __device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __restrict__ L, int n, float thr,
                                                float* sv_out, uint64_t* keys) {
     constexpr int S = BettiSmem<NP>::S;
+    // the keys go to the matrix region of the LDS while it is free (NP = 48: 576 keys, 64: 1,024,
+    // every key the sort takes), past it to scratch (NP = 32: keys 256..511)
+    constexpr int kLdsKeys = NP * S / 4;
+    uint64_t* kl = reinterpret_cast<uint64_t*>(s.D);
     const int lane = lane_id();
     const int tot = c2(n);
-    // the matrix starts as kNoCode everywhere (pairs above thr, the diagonal)
-    {
-        uint32_t* Dw = reinterpret_cast<uint32_t*>(s.D);
-        for (int w = lane; w < NP * S / 2; w += kWave) Dw[w] = (kNoCode << 16) | kNoCode;
-    }
-    // (1) compaction of the distances <= thr into scratch keys, t-order; lane l holds entries
-    // t = l + 64 u, its (i, j) advanced incrementally (entry t of the packing is row i, column
-    // t - c2(i))
+    // (1) compaction of the distances <= thr, t-order; entry t of the packing is row i, column
+    // t - c2(i), with i from the f32 root of 8t + 1 plus a 0.004 bias (exact for t < 2,016:
+    // gram_triangle_narrow)
     int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)lane)) * 0.5f);
     i -= c2(i) > lane;
     i += c2(i + 1) <= lane;
@@ -847,21 +847,38 @@ __device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __
         while (j >= i) { j -= i; ++i; }
         const bool ok0 = v0 <= thr, ok1 = v1 <= thr;
         const uint64_t b0 = ballot(ok0), b1 = ballot(ok1);
-        if (ok0 && m + mask_prefix(b0) < 1024)
-            at(keys, m + mask_prefix(b0)) = ((uint64_t)__float_as_uint(v0) << 12) | (uint64_t)((i0 << 6) | j0);
+        const int s0 = m + mask_prefix(b0);
+        const uint64_t k0 = ((uint64_t)__float_as_uint(v0) << 12) | (uint64_t)((i0 << 6) | j0);
+        if (ok0 && s0 < kLdsKeys) kl[s0] = k0;
+        else if (ok0 && s0 < kRankMax<NP>) at(keys, s0) = k0;
         m += __popcll(b0);
-        if (ok1 && m + mask_prefix(b1) < 1024)
-            at(keys, m + mask_prefix(b1)) = ((uint64_t)__float_as_uint(v1) << 12) | (uint64_t)((i1 << 6) | j1);
+        const int s1 = m + mask_prefix(b1);
+        const uint64_t k1 = ((uint64_t)__float_as_uint(v1) << 12) | (uint64_t)((i1 << 6) | j1);
+        if (ok1 && s1 < kLdsKeys) kl[s1] = k1;
+        else if (ok1 && s1 < kRankMax<NP>) at(keys, s1) = k1;
         m += __popcll(b1);
     }
     m = (int)uni((uint32_t)m);
     if (m > kRankMax<NP>) return kRankDense;
-    __syncthreads();  // the keys (scratch) are read by other lanes
+    if constexpr (kLdsKeys < kRankMax<NP>) __syncthreads();  // scratch keys are read by other lanes
+    lds_sync();
+    auto key_at = [&](int e) __attribute__((always_inline)) {
+        if constexpr (kLdsKeys >= kRankMax<NP>) return kl[e];
+        else return e < kLdsKeys ? kl[e] : at(keys, e);
+    };
+    // the matrix starts as kNoCode everywhere (pairs above thr, the diagonal)
+    auto clear = [&]() __attribute__((always_inline)) {
+        lds_sync();
+        uint32_t* Dw = reinterpret_cast<uint32_t*>(s.D);
+        for (int w = lane; w < NP * S / 2; w += kWave) Dw[w] = (kNoCode << 16) | kNoCode;
+        lds_sync();
+    };
     uint32_t z;
     if constexpr (NP <= 48) {
-        z = rank_sorted<8>(s.D, S, keys, m, sv_out, lane);
+        z = rank_sorted<8>(s.D, S, key_at, clear, m, sv_out, lane);
     } else {
-        z = m <= 512 ? rank_sorted<8>(s.D, S, keys, m, sv_out, lane) : rank_sorted<16>(s.D, S, keys, m, sv_out, lane);
+        z = m <= 512 ? rank_sorted<8>(s.D, S, key_at, clear, m, sv_out, lane)
+                     : rank_sorted<16>(s.D, S, key_at, clear, m, sv_out, lane);
     }
     lds_sync();
     return z;
