@@ -189,12 +189,12 @@ def main():
             alt = "f32" if f64 else "f64"
             roof["rbf_" + alt] = alt_rbf_measurement(ctx, sh, args, nbins, abi, dgn, torch, alt)
     dk = ktimes.get("betti_dist", {})
-    dist = None
+    dist_roof = None
     if dk.get("launches") and dk["total_ms"] > 0:
         dk_s = dk["total_ms"] / dk["launches"] / 1e3
         tfs = dk["flops"] / dk["launches"] / dk_s / 1e12
         gbs = dk["bytes"] / dk["launches"] / dk_s / 1e9
-        dist = {"bound": "valu", "kernel": "betti_dist (neighbour search + f64 Gram distances -> f32 triangles)",
+        dist_roof = {"bound": "valu", "kernel": "betti_dist (neighbour search + f64 Gram distances -> f32 triangles)",
                 "achieved": round(tfs, 6), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": tfs / FP64_PEAK_TFS, "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                 "note": ("useful 6n^2 flops per local complex (K=3 Gram); one packed pair per lane on the f64 VALU "
@@ -212,7 +212,7 @@ def main():
                    "structures_per_gpu": B, "atoms_per_structure": n_atoms, "edges_per_gpu": E,
                    "parallelism": f"shard{world}"},
         "roofline": roof,
-        "roofline_dist": dist,
+        "roofline_dist": dist_roof,
         "kernel_ms_per_step": kernel_ms,
     }
     if args.dump_shards:
