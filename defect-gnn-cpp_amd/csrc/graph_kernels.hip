@@ -47,9 +47,12 @@ __device__ __forceinline__ uint64_t pack_cell_atom(int j, int s0, int s1, int s2
            ((uint64_t)(s2 + 512) << 52);
 }
 
-// per structure: geometry + the reference image bound + search strategy
-__device__ __noinline__ StructMeta structure_meta(const double* __restrict__ lattice,
-                                                  const int64_t* __restrict__ atom_offset, int64_t b, double rc) {
+// thread per structure: geometry + the reference image bound + search strategy
+__global__ __launch_bounds__(128) void prep_meta_kernel(const double* __restrict__ lattice,
+                                                        const int64_t* __restrict__ atom_offset, int64_t B, double rc,
+                                                        StructMeta* __restrict__ meta) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
     StructMeta m;
     const double* L = lattice + 9 * b;
     for (int k = 0; k < 9; ++k) m.L[k] = L[k];
@@ -124,7 +127,7 @@ __device__ __noinline__ StructMeta structure_meta(const double* __restrict__ lat
         }
         for (int k = 0; k < 3; ++k) m.nc[k] = nc[k];
     }
-    return m;
+    meta[b] = m;
 }
 
 // fractional cell coordinate of atom position p: floor s (the periodic shift of the wrapped
@@ -141,13 +144,9 @@ __device__ __forceinline__ void frac_fixed(const double* R, int k, const double 
     W = (uint32_t)w;
 }
 
-// block per structure: its metadata (one thread; the other kernels read meta[b]), the atom ->
-// structure map, the far-position check, the per-atom 1/count(species) Betti weight and, for
-// structures above kStage atoms, the cell list (one launch: a separate metadata kernel cost a
-// launch of its own, ~4.5 us in the small-batch configs)
-__global__ __launch_bounds__(1024) void prep_atoms_kernel(const double* __restrict__ lattice,
-                                                         const int64_t* __restrict__ atom_offset, double rc,
-                                                         StructMeta* __restrict__ meta,
+// block per structure: atom -> structure map, the far-position check, the per-atom
+// 1/count(species) Betti weight and, for structures above kStage atoms, the cell list
+__global__ __launch_bounds__(1024) void prep_atoms_kernel(const StructMeta* __restrict__ meta,
                                                          const double* __restrict__ pos,
                                                          const int32_t* __restrict__ species,
                                                          int32_t* __restrict__ atom_struct,
@@ -157,15 +156,9 @@ __global__ __launch_bounds__(1024) void prep_atoms_kernel(const double* __restri
     __shared__ int32_t hist[kCellMax + 1];
     __shared__ int32_t shist[256];
     __shared__ int32_t part[1024 / kWave];
-    __shared__ StructMeta sm_s;
     const int64_t b = blockIdx.x;
     const int tid = threadIdx.x;
-    if (tid == 0) {
-        sm_s = structure_meta(lattice, atom_offset, b, rc);
-        meta[b] = sm_s;
-    }
-    __syncthreads();
-    const StructMeta& sm = sm_s;
+    const StructMeta& sm = meta[b];
     const int64_t first = sm.first;
     const int natoms = sm.natoms;
     const bool one = sm.one != 0 || sm.few != 0;  // fixed-point coordinates (10-bit floors) in use
@@ -479,7 +472,7 @@ __device__ __forceinline__ double approx_d2(const StructMeta& M, const u32x4 fq,
 // (v_pk_fma_f32); only candidates within `band32` of rc^2 (a few per thousand queries) take the
 // exact reference test in f64. The self image (j == li, n = 0) is the only image of the query
 // atom within rc. Returns m; mask[t] = the hit ballot of atom tile t (a bit per atom). The f32
-// lattice and the window [lo32, hi32] = rc^2 -+ band32 come from structure_meta (derivation
+// lattice and the window [lo32, hi32] = rc^2 -+ band32 come from prep_meta_kernel (derivation
 // there).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 // skip_self: eps > 0, so the query's own image (n = 0, d2 = 0) is skipped (neighbor_list.cpp:47); its
@@ -491,7 +484,7 @@ __device__ __forceinline__ int count_one_image(const StructMeta& M, const DGN_LD
     const int lane = lane_id();
     const int natoms = M.natoms;
     const u32x4 fq = fx[li];
-    const float lo32 = M.lo32, hi32 = M.hi32;  // structure_meta (band32 derivation there)
+    const float lo32 = M.lo32, hi32 = M.hi32;  // prep_meta_kernel (band32 derivation there)
     const float* Lf = M.lf;
     int m = 0;
 #pragma nounroll
@@ -659,7 +652,7 @@ __device__ __forceinline__ int collect_few_hits(const DGN_LDS uint64_t* mask, DG
 // e.g. config 2's SC-64 at 5 A, H = 0.54). Per axis at most two images of atom j can reach rc:
 // the nearest one (D_k of (1), image n0_k) and, when 1 - |D_k| <= H_k, the next one on the other
 // side (D_k + s_k, s_k = -sign(D_k), image n0_k + s_k) — at most 2^3 (atom, image) candidates,
-// each decided in f32 from the fixed-point fractions (window [lo32, hi32], structure_meta) with
+// each decided in f32 from the fixed-point fractions (window [lo32, hi32], prep_meta_kernel) with
 // the borderline ones sent to the exact reference test. The general search (3) enumerates the same
 // images through f64 slab bounds and per-lane image loops.
 struct FewLane {
@@ -2061,11 +2054,13 @@ hipError_t launch_prep_structures(hipStream_t s, const double* lattice, const in
                                   const int32_t* species, int64_t B, double rc, StructMeta* meta, int32_t* atom_struct,
                                   int32_t* cell_start, double4* cell_pos, double* weight, uint32_t* error_flag) {
     if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(prep_meta_kernel, dim3((unsigned)((B + 127) / 128)), dim3(128), 0, s, lattice, atom_offset, B,
+                       rc, meta);
     // block per structure; small batches (a few large cells, e.g. BASELINE config 5's supercell)
     // get 1024 threads per block for the cell-list sort
     const unsigned threads = B < 512 ? 1024u : 256u;
-    hipLaunchKernelGGL(prep_atoms_kernel, dim3((unsigned)B), dim3(threads), 0, s, lattice, atom_offset, rc, meta, pos,
-                       species, atom_struct, cell_start, cell_pos, weight, error_flag);
+    hipLaunchKernelGGL(prep_atoms_kernel, dim3((unsigned)B), dim3(threads), 0, s, meta, pos, species, atom_struct,
+                       cell_start, cell_pos, weight, error_flag);
     return hipGetLastError();
 }
 

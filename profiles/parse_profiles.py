@@ -14,7 +14,7 @@ import os
 import shutil
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# the neighbour + RBF path (bench.py roofline): prep_structures = prep_atoms (+ prep_meta before round 5)
+# the neighbour + RBF path (bench.py roofline): prep_structures = prep_meta + prep_atoms
 # (round 3: the count pass is graph_count_one_kernel + graph_count_kernel over the flagged tiles)
 PATH_KERNELS = ("prep_meta_kernel", "prep_atoms_kernel", "graph_count_one_kernel", "graph_count_kernel", "block_scan_kernel",
                 "graph_emit_kernel")
