@@ -827,9 +827,8 @@ __device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __
     uint64_t* kl = reinterpret_cast<uint64_t*>(s.D);
     const int lane = lane_id();
     const int tot = c2(n);
-    // (1) compaction of the distances <= thr, t-order; entry t of the packing is row i, column
-    // t - c2(i), with i from the f32 root of 8t + 1 plus a 0.004 bias (exact for t < 2,016:
-    // gram_triangle_narrow)
+    // (1) compaction of the distances <= thr, t-order; lane l holds entries t = l + 64 u, its
+    // (i, j) advanced incrementally (entry t of the packing is row i, column t - c2(i))
     int i = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)lane)) * 0.5f);
     i -= c2(i) > lane;
     i += c2(i + 1) <= lane;

@@ -1,5 +1,5 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out/g31
+mkdir -p gpurun_out/g33
 export TMPDIR=/tmp
-timeout -k 10 600 bash tools/ab.sh gpurun_out/g31/ab 2 pre v1 v2
+timeout -k 10 600 bash tools/ab.sh gpurun_out/g33/ab 2 pre pf
