@@ -198,7 +198,8 @@ def main():
                 "achieved": round(tfs, 6), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                 "frac": tfs / FP64_PEAK_TFS, "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
                 "note": ("useful 6n^2 flops per local complex (K=3 Gram); one packed pair per lane on the f64 VALU "
-                         "(the square root's Newton steps and the pair index are not counted): issue-bound")}
+                         "(the square root's Newton steps and the pair index are not counted; SQ counters in "
+                         "profiles/r05_dist.json)")}
 
     label = args.config or ("config4" if (args.kind, args.m) == ("fcc", 4) else f"{args.kind}{args.m}")
     result = {
