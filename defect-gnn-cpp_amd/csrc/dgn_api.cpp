@@ -948,6 +948,23 @@ int dgn_debug_host_syncs(dgn_ctx* c, int64_t* out) {
     return DGN_OK;
 }
 
+int dgn_debug_check_wide_layouts(int64_t* first_bad) {
+    if (!first_bad) return DGN_ERR_ARG;
+    *first_bad = -1;
+    auto pow2 = [](int64_t x) { return x > 0 && x <= INT32_MAX && (x & (x - 1)) == 0; };
+    for (int nmax = 65; nmax <= betti_max_points(); ++nmax)
+        for (int big = 0; big <= 1; ++big)
+            for (int grow = 0; grow <= (big ? kWideMaxGrow : 0); ++grow) {
+                const WideLayout l = betti_wide_layout(nmax, big != 0, 0, grow);
+                if (!pow2(l.na_cap) || !pow2(l.p_cap) || !pow2(l.h_cap) || !pow2(l.vs_cap) || !pow2(l.vl_cap) ||
+                    l.h_cap != 2 * (int64_t)l.na_cap || l.total <= 0) {
+                    *first_bad = (int64_t)nmax * 64 + big * 16 + grow;
+                    return DGN_ERR_INTERNAL;
+                }
+            }
+    return DGN_OK;
+}
+
 const char* dgn_ctx_last_error(const dgn_ctx* c) { return c ? c->last_error.c_str() : "null context"; }
 
 int dgn_ctx_enable_timing(dgn_ctx* c, int on) {

@@ -24,7 +24,7 @@ EXPORTS = [
     "dgn_host_persistence_lower", "dgn_host_rbf", "dgn_debug_betti_clouds", "dgn_dev_node_features",
     "dgn_dev_edge_arrays", "dgn_host_edge_arrays", "dgn_edge_arrays_free", "dgn_dev_graph_betti",
     "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug", "dgn_debug_retry_count",
-    "dgn_debug_host_syncs",
+    "dgn_debug_host_syncs", "dgn_debug_check_wide_layouts",
 ]
 DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2 = 1, 2, 3, 4, 6
 
@@ -104,6 +104,8 @@ def lib():
         L.dgn_debug_retry_count.argtypes = [vp, C.POINTER(i64)]
     if hasattr(L, "dgn_debug_host_syncs"):
         L.dgn_debug_host_syncs.argtypes = [vp, C.POINTER(i64)]
+    if hasattr(L, "dgn_debug_check_wide_layouts"):
+        L.dgn_debug_check_wide_layouts.argtypes = [C.POINTER(i64)]
     L.dgn_ctx_last_error.restype = C.c_char_p
     L.dgn_ctx_last_error.argtypes = [vp]
     L.dgn_ctx_enable_timing.argtypes = [vp, C.c_int]

@@ -80,6 +80,11 @@ int dgn_debug_retry_count(dgn_ctx* ctx, int64_t* count);
 /* Diagnostics: how many times the context's calls waited for its stream since the last call
  * (no synchronization itself; tests of the asynchronous device entry points). */
 int dgn_debug_host_syncs(dgn_ctx* ctx, int64_t* count);
+/* Diagnostics (host arithmetic only, no device, no context): every wide-kernel scratch layout the
+ * Betti pass can choose (65..2,048 points, regular and capacity-retry at every growth level) has
+ * positive power-of-two int32 table capacities. DGN_OK, or DGN_ERR_INTERNAL with *first_bad =
+ * nmax * 64 + big * 16 + grow of the first layout that does not. */
+int dgn_debug_check_wide_layouts(int64_t* first_bad);
 const char* dgn_ctx_last_error(const dgn_ctx* ctx);
 
 /* Per-kernel timing with hipEvents recorded on the launch stream around every launch. */

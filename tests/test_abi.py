@@ -60,3 +60,13 @@ def test_rbf_bins_and_defaults():
     p = L.GraphParams()
     lib.dgn_graph_params_default(p)
     assert (p.r_cutoff, p.max_neighbors, p.epsilon, p.rbf_cutoff, p.rbf_dr) == (10.0, 20, 1e-10, 10.0, 0.1)
+
+
+def test_wide_layouts_keep_power_of_two_caps():
+    """Every wide / capacity-retry scratch layout (65..2,048 points, every growth level) keeps its
+    int32 table capacities positive powers of two (the pivot hash of the last
+    growth level overflowed int32). Host arithmetic only: runs without a GPU."""
+    import ctypes
+    bad = ctypes.c_int64(0)
+    st = dgn.lib().dgn_debug_check_wide_layouts(ctypes.byref(bad))
+    assert st == 0, f"layout nmax={bad.value // 64} big={(bad.value // 16) & 1} grow={bad.value % 16}"
