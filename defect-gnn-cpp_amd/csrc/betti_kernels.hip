@@ -439,13 +439,15 @@ struct Complex {
         const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
         const int c = (int)(sp_ & 255);
         // lane k reads row entries (x, k): consecutive lanes, consecutive banks
-        uint32_t dd = max(ds, max(Db()[a * S + k], Db()[b * S + k]));
+        // (u32 operands throughout: a u32 / u16 max resolves to the double overload, three f64
+        // conversions and a v_max_f64 per cofacet)
+        uint32_t dd = max(ds, max((uint32_t)Db()[a * S + k], (uint32_t)Db()[b * S + k]));
         uint32_t sel;
         if (dim == 1) {
             // ~(k,a,b) / ~(a,k,b) / ~(a,b,k); the top byte of ~pack3 is 0xFF (S1 byte 2 of ~sp_)
             sel = k > a ? 0x02040100u : (k > b ? 0x02010400u : 0x02010004u);
         } else {
-            dd = max(dd, Db()[c * S + k]);
+            dd = max(dd, (uint32_t)Db()[c * S + k]);
             sel = k > a ? 0x04020100u : (k > b ? 0x02040100u : (k > c ? 0x02010400u : 0x02010004u));
         }
         const uint32_t nk = __builtin_amdgcn_perm(kc, ~sp_, sel);
