@@ -145,9 +145,12 @@ struct WideCx {
 
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
+    // d(i, j) at a per-lane (i, j): scalar matrix base + 32-bit element offset (i n + j < 2^22), not
+    // a 64-bit vector address built from a 64-bit product per read
     __device__ uint32_t d(int i, int j) const {
-        if (MODE == kC16) return sp<uint16_t>(ly.D)[(int64_t)i * n + j];
-        return sp<uint32_t>(ly.D)[(int64_t)i * n + j];
+        const uint32_t ix = (uint32_t)i * (uint32_t)n + (uint32_t)j;
+        if (MODE == kC16) return at(sp<uint16_t>(ly.D), ix);
+        return at(sp<uint32_t>(ly.D), ix);
     }
     __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
     // d(a, x) for a wave-uniform row a: scalar row base + 32-bit lane offset
@@ -418,12 +421,12 @@ struct WideCx {
                         // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet:
                         // the facets with k replacing a larger vertex must be strictly shorter
                         const bool app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
-                        if (app) mc_t[pidx(3, bestp)] = kMcClearedW;  // clearing for dim 2
+                        if (app) at(mc_t, (uint32_t)pidx(3, bestp)) = kMcClearedW;  // clearing for dim 2
                         else na = true;
                         mc = (uint16_t)bk;
                     }
                 }
-                mc_e[bin2(i) + j] = mc;
+                at(mc_e, (uint32_t)(bin2(i) + j)) = mc;
             }
             // apparent pairs have zero persistence: nothing to emit
             na_append(0, na, nna, colkey, best, bestp, colp);
@@ -553,7 +556,7 @@ struct WideCx {
                 }
                 bool cleared = false;
                 if (fresh) {
-                    cleared = mc_t[tidx] == kMcClearedW;
+                    cleared = at(mc_t, (uint32_t)tidx) == kMcClearedW;
                     dab = d(a, b);
                     dac = d(a, c);
                     dbc = d(b, c);
@@ -562,7 +565,7 @@ struct WideCx {
                 }
                 bool done;
                 if (cleared) {
-                    mc_t[tidx] = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
+                    at(mc_t, (uint32_t)tidx) = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
                     done = true;
                 } else {
                     // (diameter, k) only, as in min_cofacet: a smaller k wins only with a strictly
@@ -598,7 +601,7 @@ struct WideCx {
                             na = !app;
                             mc = (uint16_t)bk;
                         }
-                        mc_t[tidx] = mc;
+                        at(mc_t, (uint32_t)tidx) = mc;
                         colkey = wkey(ds, tidx);
                         ntau = best;
                         ntv = bestp;
@@ -633,7 +636,7 @@ struct WideCx {
                 bool cl = false;
                 if (i < cnt) {
                     const uint64_t idx = ~K[i] & ((1ull << KS) - 1);
-                    cl = mc_t[idx] == kMcClearedW;
+                    cl = at(mc_t, (uint32_t)idx) == kMcClearedW;
                     if (cl) K[i] = 0ull;
                 }
                 kept -= __popcll(ballot(cl));
@@ -781,7 +784,8 @@ struct WideCx {
                 drop = t;
             }
         }
-        const uint16_t m = dim == 1 ? sp<uint16_t>(ly.mc_e)[pidx(2, bestf)] : sp<uint16_t>(ly.mc_t)[pidx(3, bestf)];
+        const uint16_t m = dim == 1 ? at(sp<uint16_t>(ly.mc_e), (uint32_t)pidx(2, bestf))
+                                     : at(sp<uint16_t>(ly.mc_t), (uint32_t)pidx(3, bestf));
         const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
         if (uniw(m) == (uint32_t)vd) app = (PT)bestf;
         return kNoMetaW;
@@ -1002,7 +1006,7 @@ struct WideCx {
             if (dim == 1) {  // clearing: tau's column is zero in dim 2 (reset after the dim-2 sort)
                 const uint64_t ti = pidx(3, tv);
                 if (lane == 0) {
-                    sp<uint16_t>(ly.mc_t)[ti] = kMcClearedW;
+                    at(sp<uint16_t>(ly.mc_t), (uint32_t)ti) = kMcClearedW;
                     sp<uint32_t>(ly.cl_list)[ncl] = (uint32_t)ti;
                 }
                 ++ncl;
@@ -1100,7 +1104,7 @@ struct WideCx {
         // (every other min-cofacet entry a later complex reads is rewritten by its dim-2 pass)
         uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
         const uint32_t* cl = sp<uint32_t>(ly.cl_list);
-        for (int i = lane_id(); i < ncl; i += kWave) mc_t[cl[i]] = kMcNoneW;
+        for (int i = lane_id(); i < ncl; i += kWave) at(mc_t, cl[i]) = kMcNoneW;
         wave_scratch_sync();
         const bool ok = finish(gi, weight);
         wave_scratch_sync();
