@@ -149,6 +149,7 @@ struct dgn_ctx {
     int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
     int dbg_big_log2 = 0;          // capacity-retry layout's first-level table size log2 (0 = natural 24)
+    int dbg_emit_chunk = 0;        // tiles per launch of the large-row emit (0 = the byte budget's)
     // host staging
     DevBuf h_lat, h_pos, h_spec, h_off;
     DevBuf dist_scratch;  // emit distance rows when the caller wants an RBF but no distances
@@ -417,7 +418,7 @@ int graph_emit_impl(dgn_ctx* c, const dgn_batch* b, const int64_t* row_ptr, int3
         TimedLaunch t(c, "graph_emit", bytes, 0);
         HIP_TRY(c, launch_graph_emit(c->stream, g, cap, stage, W.counts.as<int32_t>(), W.block_sums.as<int64_t>(),
                                      const_cast<int64_t*>(row_ptr), col, dist_rows, disp, rbf, rs, &sc->graph_flag,
-                                     key_rows, W.max_candidates));
+                                     key_rows, W.max_candidates, c->dbg_emit_chunk));
     }
     HIP_TRY(c, hipMemcpyAsync(&c->host->emit_flag, &sc->graph_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     c->emit_pending = true;
@@ -917,6 +918,7 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
         case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
         case DGN_DEBUG_WIDE_CAP: c->dbg_wide_cap = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_BIG_LOG2: c->dbg_big_log2 = value > 0 && value < 24 ? value : 0; return DGN_OK;
+        case DGN_DEBUG_EMIT_CHUNK: c->dbg_emit_chunk = value > 0 ? value : 0; return DGN_OK;
         default: return fail(c, DGN_ERR_ARG, "dgn_ctx_set_debug: unknown knob " + std::to_string(knob));
     }
 }

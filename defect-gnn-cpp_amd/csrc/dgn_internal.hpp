@@ -82,7 +82,7 @@ int64_t emit_key_rows_per_chunk(uint32_t max_candidates);
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rbf_spec, uint32_t* error_flag,
-                             double* key_rows = nullptr, uint32_t max_candidates = 0);
+                             double* key_rows = nullptr, uint32_t max_candidates = 0, int chunk_tiles = 0);
 
 hipError_t launch_rbf(hipStream_t s, const double* d, int64_t E, const RbfSpec& rs, int layout, void* out);
 

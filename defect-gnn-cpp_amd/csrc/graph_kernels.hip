@@ -1656,6 +1656,7 @@ struct EmitTiles {
 struct EmitKeys {
     double* base;
     int32_t cap;
+    int32_t chunk;  // tiles per launch (host side; 0 = emit_key_chunk_tiles)
 };
 
 template <int CAP, bool STREAM>
@@ -2131,7 +2132,8 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
     };
     if (CAP == 0) {
         // global key rows: one row per wave of a chunk of emit_key_chunk_tiles tiles, launched in turn
-        const int64_t chunk = emit_key_chunk_tiles((uint32_t)gk.cap);
+        const int64_t chunk = gk.chunk > 0 ? std::min<int64_t>(gk.chunk, emit_key_chunk_tiles((uint32_t)gk.cap))
+                                           : emit_key_chunk_tiles((uint32_t)gk.cap);
         for (int64_t t0 = 0; t0 < nt; t0 += chunk) go({t0, std::min<int64_t>(chunk, nt - t0), 0, 0, fused});
         return;
     }
@@ -2144,11 +2146,11 @@ static void launch_emit_t(hipStream_t s, const GraphLaunch& g, int stage, const 
 hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int stage, const int32_t* counts,
                              const int64_t* block_offsets, int64_t* row_ptr, int32_t* col, double* dist,
                              double* disp, void* rbf, const RbfSpec& rs, uint32_t* error_flag, double* key_rows,
-                             uint32_t max_candidates) {
+                             uint32_t max_candidates, int chunk_tiles) {
     const int64_t nb = graph_blocks(g.num_atoms, g.qa);
     if (nb <= 0) return hipSuccess;
     const bool stream = g.kmax <= (uint64_t)kStreamMaxK;
-    EmitKeys gk{nullptr, 0};
+    EmitKeys gk{nullptr, 0, 0};
 #define DGN_EMIT(C)                                                                                              \
     case C:                                                                                                      \
         if (stream) launch_emit_t<C, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs, \
@@ -2169,7 +2171,7 @@ hipError_t launch_graph_emit(hipStream_t s, const GraphLaunch& g, int cap, int s
             break;
         case kEmitGlobalKeys:
             if (!key_rows) return hipErrorInvalidValue;
-            gk = {key_rows, (int32_t)((emit_key_row_doubles(max_candidates) - 1) / 3)};
+            gk = {key_rows, (int32_t)((emit_key_row_doubles(max_candidates) - 1) / 3), chunk_tiles};
             if (stream) launch_emit_t<0, true>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,
                                                error_flag, gk);
             else launch_emit_t<0, false>(s, g, stage, counts, block_offsets, row_ptr, col, dist, disp, rbf, rs,

@@ -26,7 +26,7 @@ EXPORTS = [
     "dgn_synth_atoms_per_structure", "dgn_synth_batch", "dgn_ctx_set_debug", "dgn_debug_retry_count",
     "dgn_debug_host_syncs", "dgn_debug_check_wide_layouts",
 ]
-DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2 = 1, 2, 3, 4, 6
+DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2, DEBUG_EMIT_CHUNK = 1, 2, 3, 4, 6, 7
 
 
 class DgnError(RuntimeError):

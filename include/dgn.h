@@ -65,14 +65,18 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  *                        kernel and take the in-kernel capacity-retry path; 0 = the natural caps;
  * DGN_DEBUG_BIG_LOG2     > 0: the capacity-retry layout's first level holds 2^value-entry column /
  *                        pivot / pair tables and V store (default 2^24), so ordinary complexes outgrow it
- *                        and are reduced again at the next levels (4x the tables each); 0 = natural. */
+ *                        and are reduced again at the next levels (4x the tables each); 0 = natural;
+ * DGN_DEBUG_EMIT_CHUNK   > 0: the large-row graph emit (per-wave key rows in HBM) launches this many
+ *                        tiles at a time instead of its byte budget's count (its chunk loop on small
+ *                        inputs); 0 = natural. */
 enum {
     DGN_DEBUG_FORCE_RETRY = 1,
     DGN_DEBUG_WIDE_WAVES = 2,
     DGN_DEBUG_WIDE_C16 = 3,
     DGN_DEBUG_WIDE_CAP = 4,
     /* 5: removed (the round-3 workgroup-per-complex kernel) */
-    DGN_DEBUG_BIG_LOG2 = 6
+    DGN_DEBUG_BIG_LOG2 = 6,
+    DGN_DEBUG_EMIT_CHUNK = 7
 };
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 /* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */

@@ -267,6 +267,26 @@ def test_fcc256_large_rows_global_keys(ctx, rc, k):
     check_rbf(g["rbf"], dist, rc, 0.5)
 
 
+def test_large_rows_chunked_launches(ctx):
+    """The global-key emit's chunk loop: key rows are reused launch after launch, a few tiles at a
+    time (DGN_DEBUG_EMIT_CHUNK = 3 instead of the 256 MB budget's count, which covers a single
+    structure in one launch). FCC-256 at 17 A, K = inf: CSR, distances and displacements bit-exact
+    vs the oracle."""
+    batch = dgn.synth_batch("fcc", 4, 1)
+    p = abi.graph_params(r_cutoff=17.0, max_neighbors=None, rbf_cutoff=17.0, rbf_dr=0.5, write_displacement=True)
+    ctx.set_debug(abi.DEBUG_EMIT_CHUNK, 3)
+    try:
+        g = ctx.host_graph(batch, p)
+    finally:
+        ctx.set_debug(abi.DEBUG_EMIT_CHUNK, 0)
+    rp, col, dist, disp = oracle_batch_csr(batch, 17.0, None)
+    assert np.array_equal(g["row_ptr"], rp)
+    assert np.array_equal(g["col"], col)
+    assert np.array_equal(g["dist"], dist)
+    assert np.array_equal(g["disp"], disp)
+    check_rbf(g["rbf"], dist, 17.0, 0.5)
+
+
 @pytest.mark.parametrize("k", [20, None])
 def test_fcc256_cutoff_12A_above_512_candidates(ctx, k):
     """NeighborList(rc = 12): ~580 candidates per atom (the 1,024-candidate emit), CSR bit-exact."""
