@@ -18,7 +18,8 @@ HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I$T -Iinclude 
 rm -f "$B"/*.o
 pids=()
 for f in graph_kernels betti_kernels betti_wide betti_rank betti_split node_kernels; do
-  /opt/rocm/bin/hipcc $HF -c "$T/$f.hip" -o "$B/$f.o" & pids+=($!)
+  PF=""; [ "$f" = betti_kernels ] && PF="-mllvm -amdgpu-sched-strategy=iterative-minreg"  # Makefile per-source flag
+  /opt/rocm/bin/hipcc $HF $PF -c "$T/$f.hip" -o "$B/$f.o" & pids+=($!)
 done
 /opt/rocm/bin/hipcc $HF -x hip -c "$T/dgn_api.cpp" -o "$B/dgn_api.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done

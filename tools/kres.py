@@ -16,8 +16,10 @@ KEYS = {"TotalSGPRs": "sgpr", "VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [by
         "Occupancy [waves/SIMD]": "occ", "SGPRs Spill": "sgpr_spill", "VGPRs Spill": "vgpr_spill",
         "LDS Size [bytes/block]": "lds"}
 print(f"{'kernel':70s} {'vgpr':>5s} {'sgpr':>5s} {'vspill':>6s} {'sspill':>6s} {'scratch':>7s} {'lds':>7s} {'occ':>4s}")
+# per-source flags of the Makefile
+PER_SRC = {"betti_kernels.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]}
 for src in args:
-    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + extra + ["-c", src, "-o", "/tmp/kres.o"]
+    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + PER_SRC.get(src.split("/")[-1], []) + extra + ["-c", src, "-o", "/tmp/kres.o"]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
     for line in out.splitlines():
