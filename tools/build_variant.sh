@@ -15,7 +15,7 @@ for f in $SRCS; do
   if [ "$f" = dgn_api ]; then
     /opt/rocm/bin/hipcc $HF -x hip -c defect-gnn-cpp_amd/csrc/dgn_api.cpp -o $B/dgn_api.o &
   else
-    PF=""; [ "$f" = betti_kernels ] && PF="-mllvm -amdgpu-sched-strategy=iterative-minreg"  # Makefile per-source flag
+    PF=""; [ "$f" = betti_kernels ] && [[ "$FLAGS" != *sched-strategy* ]] && PF="-mllvm -amdgpu-sched-strategy=iterative-minreg"  # Makefile per-source flag
     /opt/rocm/bin/hipcc $HF $PF -c defect-gnn-cpp_amd/csrc/$f.hip -o $B/$f.o &
   fi
 done
