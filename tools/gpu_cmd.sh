@@ -1,10 +1,7 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-mkdir -p gpurun_out/g55
+mkdir -p gpurun_out/g56
 export TMPDIR=/tmp
-bash tools/ab.sh gpurun_out/g55/ab 2 base gkilp gkmc
-for tag in base bwmc bwilp base bwmc bwilp; do
-  lib=defect-gnn-cpp_amd/lib/libdgn.so; [ "$tag" != base ] && lib=defect-gnn-cpp_amd/lib/libdgn_$tag.so
-  echo "== $tag"
-  DGN_LIB=$lib timeout -k 10 300 python -u tools/betti_rc10.py 64 2 2>&1 | grep "rep 1" || exit 1
-done
+DGN_LIB=defect-gnn-cpp_amd/lib/libdgn_st5.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_betti.py tests/test_gpu_betti_cellist.py -m gpu > gpurun_out/g56/tests.txt 2>&1 || { tail -30 gpurun_out/g56/tests.txt; exit 1; }
+tail -2 gpurun_out/g56/tests.txt
+bash tools/ab.sh gpurun_out/g56/ab 3 base st4 st5
