@@ -846,7 +846,9 @@ __device__ __forceinline__ uint32_t rank_codes(BettiSmem<NP>& s, const float* __
         const int i1 = i, j1 = j;
         j += kWave;
         while (j >= i) { j -= i; ++i; }
-        const bool ok0 = v0 <= thr, ok1 = v1 <= thr;
+        // padding lanes past the triangle (t >= tot) never count as edges, even at thr = +inf:
+        // their (i, j) run past n and a mirrored store would overwrite real codes
+        const bool ok0 = t < tot && v0 <= thr, ok1 = t + kWave < tot && v1 <= thr;
         const uint64_t b0 = ballot(ok0), b1 = ballot(ok1);
         const int s0 = m + mask_prefix(b0);
         const uint64_t k0 = ((uint64_t)__float_as_uint(v0) << 12) | (uint64_t)((i0 << 6) | j0);

@@ -83,7 +83,7 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 // MODE: kF32 (distances as f32 bits), kC16 (u16 rank codes: 4-byte -> 2-byte matrix for
 // complexes of <= 362 points, C(362, 2) < 2^16), kBig, kHuge (above).
 constexpr int kF32 = 0, kC16 = 1, kBig = 2, kHuge = 3;
-template <int KW, int MODE>
+template <int KW, int MODE, bool PRE = false>
 struct WideCx {
     static constexpr bool BIG = MODE == kBig;
     static constexpr bool HUGE = MODE == kHuge;
@@ -120,6 +120,10 @@ struct WideCx {
     }
     __device__ static uint32_t kdiam(uint64_t key) { return (uint32_t)(key >> KS); }
     __device__ static uint32_t pack_edge(int i, int j) { return ((uint32_t)i << VB) | (uint32_t)j; }
+    // PRE (u16 codes after the walk pass, betti_walk_kernel): the matrix, the bitsets, the threshold
+    // code and the dim-2 column list come from bl.walk; clearing marks live in a bitmap (ly.clb)
+    // and the dim-2 apparent owners are decided from the matrix (lookup) -- no min-cofacet table
+    static_assert(!PRE || MODE == kC16, "the walk pass covers the u16-coded complexes");
     const BettiLaunch& bl;
     const WideLayout& ly;
     uint64_t* adj;  // LDS [n][W]: row v = the neighbours of vertex v, W words
@@ -141,7 +145,19 @@ struct WideCx {
     // an all-ones diagonal excluding the simplex's own vertices
     uint32_t thrc = 0;
 
+    const uint8_t* dm = nullptr;  // the distance matrix: this wave's scratch (ly.D) or PRE the walk pass's
+    int64_t wslot = 0;            // the complex's slice position (PRE: its walk-pass outputs)
+    uint16_t* mce = nullptr;      // dim-1 min-cofacet table: scratch (ly.mc_e) or PRE the walk pass's
+    float* d0p = nullptr;         // dim-0 deaths: scratch (ly.d0) or PRE the walk pass's
+
     __device__ float value(uint32_t dc) const { return CODED ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
+    // cleared-triangle bitmap (PRE): set / test bit t
+    __device__ uint32_t* clbits() const { return sp<uint32_t>(ly.clb); }
+    __device__ void clear_mark(uint32_t t) const { atomicOr(&at(clbits(), t >> 5), 1u << (t & 31)); }
+    // (the marks are L2 atomics: read past the CU's L1, which may hold a stale copy of the word)
+    __device__ bool is_cleared(uint32_t t) const {
+        return (__hip_atomic_load(&at(clbits(), t >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (t & 31)) & 1u;
+    }
 
     template <class T>
     __device__ T* sp(int64_t off) const { return reinterpret_cast<T*>(scr + off); }
@@ -149,15 +165,15 @@ struct WideCx {
     // a 64-bit vector address built from a 64-bit product per read
     __device__ uint32_t d(int i, int j) const {
         const uint32_t ix = (uint32_t)i * (uint32_t)n + (uint32_t)j;
-        if (MODE == kC16) return at(sp<uint16_t>(ly.D), ix);
-        return at(sp<uint32_t>(ly.D), ix);
+        if (MODE == kC16) return at(reinterpret_cast<const uint16_t*>(dm), ix);
+        return at(reinterpret_cast<const uint32_t*>(dm), ix);
     }
     __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
     // d(a, x) for a wave-uniform row a: scalar row base + 32-bit lane offset
     __device__ uint32_t drow(int a, uint32_t x) const {
         const uint32_t ra = (uint32_t)a * (uint32_t)n;
-        if (MODE == kC16) return at(sp<uint16_t>(ly.D) + ra, x);
-        return at(sp<uint32_t>(ly.D) + ra, x);
+        if (MODE == kC16) return at(reinterpret_cast<const uint16_t*>(dm) + ra, x);
+        return at(reinterpret_cast<const uint32_t*>(dm) + ra, x);
     }
     // u16 codes (n <= 362, 9-bit vertices): the pivot search compares cofacets by the packed-tuple
     // key (code << 36) | ~tuple, order-isomorphic to (code << 32) | ~index (a tuple packed
@@ -177,6 +193,12 @@ struct WideCx {
     // ---- distance matrix (mirrored from the packed lower triangle) + adjacency bitsets ----
     __device__ void load(int64_t gi, int64_t slot) {
         const int lane = lane_id();
+        if constexpr (PRE) {  // the walk pass built the matrix and the threshold code
+            (void)gi;
+            (void)lane;
+            thrc = uniw(bl.walk.meta[8 * slot + kWmThr]);
+            return;
+        }
         const float* L = bl.lower + gi * bl.tri_stride;
         uint32_t* D = sp<uint32_t>(ly.D);
         uint16_t* D16 = sp<uint16_t>(ly.D);
@@ -619,14 +641,21 @@ struct WideCx {
     // ---- non-apparent columns in Ripser's order: bitonic sort, key descending ----
     // dim 2 (`cleared`): columns whose triangle is the pivot of a reduced dim-1 column (clearing
     // marks, set after this list was built) get key 0 and sort last; returns the columns kept
+    // the column arrays of one dimension (this wave's scratch from `base`)
+    __device__ void na_arrays(int dim, int base, uint64_t*& K, uint64_t*& T, uint64_t*& V, PT*& Cc) const {
+        (void)dim;
+        K = sp<uint64_t>(ly.na_key) + base;
+        T = sp<uint64_t>(ly.na_tau) + base;
+        V = sp<uint64_t>(ly.na_tv) + base;
+        Cc = sp<PT>(ly.na_col) + base;
+    }
     __device__ int sort_na(int base, int cnt, bool cleared) {
         const int lane = lane_id();
         int N = 1;
         while (N < cnt) N <<= 1;
-        uint64_t* K = sp<uint64_t>(ly.na_key) + base;
-        uint64_t* T = sp<uint64_t>(ly.na_tau) + base;
-        uint64_t* V = sp<uint64_t>(ly.na_tv) + base;
-        PT* Cc = sp<PT>(ly.na_col) + base;
+        uint64_t *K, *T, *V;
+        PT* Cc;
+        na_arrays(cleared ? 2 : 1, base, K, T, V, Cc);
         for (int i = cnt + lane; i < N; i += kWave) K[i] = 0ull;  // padding sorts last
         int kept = cnt;
         if (cleared) {
@@ -636,7 +665,8 @@ struct WideCx {
                 bool cl = false;
                 if (i < cnt) {
                     const uint64_t idx = ~K[i] & ((1ull << KS) - 1);
-                    cl = at(mc_t, (uint32_t)idx) == kMcClearedW;
+                    if constexpr (PRE) cl = is_cleared((uint32_t)idx);
+                    else cl = at(mc_t, (uint32_t)idx) == kMcClearedW;
                     if (cl) K[i] = 0ull;
                 }
                 kept -= __popcll(ballot(cl));
@@ -784,9 +814,41 @@ struct WideCx {
                 drop = t;
             }
         }
-        const uint16_t m = dim == 1 ? at(sp<uint16_t>(ly.mc_e), (uint32_t)pidx(2, bestf))
-                                     : at(sp<uint16_t>(ly.mc_t), (uint32_t)pidx(3, bestf));
         const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
+        if constexpr (PRE) {
+            if (dim == 2) {
+                // tau = f u {vd} with diam f = diam tau (f is its F-max facet), so vd is a
+                // zero-persistence cofacet vertex of f, and tau is f's F-minimal cofacet -- the
+                // pass_dim2 walk's winner -- iff no vertex x > vd, x not in f, has every distance
+                // to f within diam f (the all-ones diagonal excludes f's vertices). Decided from
+                // f's three rows (coalesced), words from vd's on; such a pair is always apparent
+                // (diam tau = diam f and f its F-max facet), and a cleared f (a dim-1 pivot) is
+                // never in one, so no min-cofacet table or clearing state is needed.
+                const int fa = pv(bestf, 2), fb = pv(bestf, 1), fc = pv(bestf, 0);
+                const uint32_t fd = kdiam(bestk);
+                const int t0 = vd >> 6;
+                uint32_t ra[KW], rb[KW], rc[KW];
+#pragma unroll
+                for (int t = 0; t < KW; ++t) {
+                    if (t < t0 || t >= W) continue;
+                    const uint32_t x = (uint32_t)min(64 * t + lane, n - 1);
+                    ra[t] = drow(fa, x);
+                    rb[t] = drow(fb, x);
+                    rc[t] = drow(fc, x);
+                }
+                bool later = false;
+#pragma unroll
+                for (int t = 0; t < KW; ++t) {
+                    if (t < t0 || t >= W) continue;
+                    const int x = 64 * t + lane;
+                    later |= x > vd && x < n && max(max(ra[t], rb[t]), rc[t]) <= fd;
+                }
+                if (!ballot(later)) app = (PT)bestf;
+                return kNoMetaW;
+            }
+        }
+        const uint16_t m = dim == 1 ? at(mce, (uint32_t)pidx(2, bestf))
+                                     : at(sp<uint16_t>(ly.mc_t), (uint32_t)pidx(3, bestf));
         if (uniw(m) == (uint32_t)vd) app = (PT)bestf;
         return kNoMetaW;
     }
@@ -946,10 +1008,9 @@ struct WideCx {
             return;
         }
         nna = sort_na(base, nna, dim == 2);
-        const uint64_t* K = sp<uint64_t>(ly.na_key) + base;
-        const uint64_t* T = sp<uint64_t>(ly.na_tau) + base;
-        const uint64_t* V = sp<uint64_t>(ly.na_tv) + base;
-        const PT* Cc = sp<PT>(ly.na_col) + base;
+        uint64_t *K, *T, *V;
+        PT* Cc;
+        na_arrays(dim, base, K, T, V, Cc);
         PT* vstore = sp<PT>(ly.vstore);
         float2* pairs = sp<float2>(dim == 1 ? ly.p1 : ly.p2);
         int& np = dim == 1 ? n_p1 : n_p2;
@@ -1006,8 +1067,9 @@ struct WideCx {
             if (dim == 1) {  // clearing: tau's column is zero in dim 2 (reset after the dim-2 sort)
                 const uint64_t ti = pidx(3, tv);
                 if (lane == 0) {
-                    at(sp<uint16_t>(ly.mc_t), (uint32_t)ti) = kMcClearedW;
-                    sp<uint32_t>(ly.cl_list)[ncl] = (uint32_t)ti;
+                    if constexpr (PRE) clear_mark((uint32_t)ti);
+                    else at(sp<uint16_t>(ly.mc_t), (uint32_t)ti) = kMcClearedW;
+                    if (!PRE || ncl < ly.na_cap) sp<uint32_t>(ly.cl_list)[ncl] = (uint32_t)ti;
                 }
                 ++ncl;
             }
@@ -1062,7 +1124,7 @@ struct WideCx {
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
             return false;
         }
-        const float* d0s = sp<float>(ly.d0);
+        const float* d0s = d0p;
         const float2* P1 = sp<float2>(ly.p1);
         const float2* P2 = sp<float2>(ly.p2);
         const double myval = betti_stats35(d0s, n_d0, P1, n_p1, P2, n_p2, weight);
@@ -1089,11 +1151,75 @@ struct WideCx {
     int nna1 = 0, nna2 = 0, base2 = 0, ncl = 0;
     __device__ void apparent(int64_t gi, int64_t slot) {
         load(gi, slot);
+        if constexpr (PRE) {
+            apparent_from_walk(slot);
+            return;
+        }
         prim();
         const int n_edges = edge_list();
         nna1 = pass_dim1(n_edges);
         base2 = pow2ceil(nna1);
         nna2 = pass_dim2(n_edges, base2);
+    }
+    // PRE: the walk pass's lists into this wave's column arrays (dim 1 at 0, dim 2 at base2) with
+    // their keys, initial pivots and cofacet tuples (the diameters from the matrix); the triangles the
+    // dim-1 apparent pairs clear marked in the bitmap first, and dropped from the dim-2 list (most of
+    // it at 10 A) instead of being sorted
+    __device__ void apparent_from_walk(int64_t slot) {
+        const int lane = lane_id();
+        const WalkOut& wo = bl.walk;
+        const uint32_t* meta = wo.meta + 8 * slot;
+        n_d0 = (int)uniw(meta[kWmD0]);
+        n_inf0 = (int)uniw(meta[kWmInf0]);
+        const int n1 = (int)uniw(meta[kWmNa1]), ncw = (int)uniw(meta[kWmCl]), nw = (int)uniw(meta[kWmNa2]);
+        if (n1 > wo.cap1 || ncw > wo.cap1 || nw > wo.cap || pow2ceil(n1) + pow2ceil(nw) > ly.na_cap) {
+            err |= kENA;  // a list that overflowed: capacity retry
+            return;
+        }
+        const uint32_t* CL = wo.cl + slot * (int64_t)wo.cap1;
+        for (int i = lane; i < ncw; i += kWave) clear_mark(CL[i]);
+        uint64_t* K = sp<uint64_t>(ly.na_key);
+        uint64_t* T = sp<uint64_t>(ly.na_tau);
+        uint64_t* V = sp<uint64_t>(ly.na_tv);
+        PT* Cc = sp<PT>(ly.na_col);
+        const uint64_t* E1 = wo.e1 + slot * (int64_t)wo.cap1;
+        for (int i = lane; i < n1; i += kWave) {
+            const uint64_t e = E1[i];
+            const uint32_t ed = (uint32_t)(e & ((1u << 18) - 1u));
+            const int bk = (int)((e >> 18) & VM);
+            const uint32_t bd = (uint32_t)(e >> 27);
+            const int a = (int)(ed >> VB), b = (int)(ed & VM);
+            const uint64_t bestp = pinsert(2, ed, bk);
+            K[i] = wkey(d(a, b), bin2(a) + b);
+            T[i] = wkey(bd, pidx(3, bestp));
+            V[i] = bestp;
+            Cc[i] = (PT)ed;
+        }
+        nna1 = n1;
+        base2 = pow2ceil(n1);
+        wave_scratch_sync();  // the marks (L2 atomics) before the tests below
+        const uint64_t* E = wo.ent + slot * (int64_t)wo.cap;
+        nna2 = 0;
+        for (int i0 = 0; i0 < nw; i0 += kWave) {
+            const int i = i0 + lane;
+            const uint64_t e = i < nw ? E[i] : 0ull;
+            const uint32_t colp = (uint32_t)(e & ((1u << 27) - 1u));
+            const uint32_t ti = (uint32_t)pidx(3, colp);
+            const bool keep = i < nw && !is_cleared(ti);
+            const uint64_t kb = ballot(keep);
+            if (keep) {
+                const int q = base2 + nna2 + mask_prefix(kb);
+                const int bk = (int)((e >> 27) & VM);
+                const uint32_t bd = (uint32_t)(e >> 36);
+                const uint64_t bestp = pinsert(3, colp, bk);
+                K[q] = wkey(sdiam(2, colp), ti);
+                T[q] = wkey(bd, pidx(4, bestp));
+                V[q] = bestp;
+                Cc[q] = (PT)colp;
+            }
+            nna2 += __popcll(kb);
+        }
+        wave_scratch_sync();
     }
     // Phase 2, from scratch alone (no LDS): the two reductions, the statistics and the outputs.
     // True when the complex's outputs were written.
@@ -1102,9 +1228,22 @@ struct WideCx {
         if (err == 0u) reduce(2, nna2, base2);
         // the dim-1 clearing marks were read by the dim-2 sort; reset them for the next complex
         // (every other min-cofacet entry a later complex reads is rewritten by its dim-2 pass)
-        uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
         const uint32_t* cl = sp<uint32_t>(ly.cl_list);
-        for (int i = lane_id(); i < ncl; i += kWave) at(mc_t, cl[i]) = kMcNoneW;
+        if constexpr (PRE) {
+            // every set bit of the bitmap is listed (a word shared by two entries is zeroed twice)
+            const int64_t words = ((int64_t)c2i(n) * (n - 2) / 3 + 31) / 32 + 1;
+            const int ncw = (int)uniw(bl.walk.meta[8 * wslot + kWmCl]);
+            if (ncl > ly.na_cap || ncw > bl.walk.cap1) {
+                for (int64_t i = lane_id(); i < words; i += kWave) at(clbits(), (uint32_t)i) = 0u;
+            } else {
+                const uint32_t* CL = bl.walk.cl + wslot * (int64_t)bl.walk.cap1;
+                for (int i = lane_id(); i < ncl; i += kWave) at(clbits(), cl[i] >> 5) = 0u;
+                for (int i = lane_id(); i < ncw; i += kWave) at(clbits(), CL[i] >> 5) = 0u;
+            }
+        } else {
+            uint16_t* mc_t = sp<uint16_t>(ly.mc_t);
+            for (int i = lane_id(); i < ncl; i += kWave) at(mc_t, cl[i]) = kMcNoneW;
+        }
         wave_scratch_sync();
         const bool ok = finish(gi, weight);
         wave_scratch_sync();
@@ -1112,7 +1251,7 @@ struct WideCx {
     }
 };
 
-template <int KW, int MODE>
+template <int KW, int MODE, bool PRE = false>
 __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const WideLayout& ly) {
     // dynamic LDS (wide_lds_bytes), one buffer per workgroup of kWideWaves waves: the buffer token
     // (u64), the adjacency [nmax][ceil(nmax / 64)] u64 and the forest parents [nmax] u16 (HUGE:
@@ -1150,8 +1289,12 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
             if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
             if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
         } else {
-            WideCx<KW, MODE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+            WideCx<KW, MODE, PRE> cx{bl, ly, adj, par, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
             if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+            cx.wslot = wi;
+            cx.dm = scr + ly.D;
+            cx.mce = reinterpret_cast<uint16_t*>(scr + ly.mc_e);
+            cx.d0p = reinterpret_cast<float*>(scr + ly.d0);
             // take the buffer: every lane tries the same compare-and-swap, the wave holds it when one
             // of its lanes won (a uniform ballot; no branch on the lane, see the dequeue)
             for (;;) {
@@ -1178,22 +1321,448 @@ __global__ __launch_bounds__(kWave * kWideWaves) void betti_wide_kernel(BettiLau
 #endif
 // the u16-code instantiations (the 10 A path) with a register budget for DGN_WIDE_C16_WAVES waves
 // per SIMD: resident waves are what this latency-bound kernel scales with
+// After the walk pass (u16 codes): the reductions, the statistics and the outputs only, from the
+// walk pass's per-complex outputs and this wave's scratch -- no LDS, so residency is set by registers
 template <int KW>
+__device__ __forceinline__ void betti_reduce_body(const BettiLaunch& bl, const WideLayout& ly) {
+    const int lane = lane_id();
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int64_t slot = (int64_t)blockIdx.x * kWideWaves + w;
+    if (slot >= ly.slots) return;
+    uint8_t* scr = ly.base + slot * ly.total;
+    const int64_t total = (int64_t)*bl.wide_len;
+    for (;;) {
+        const uint32_t ticket = atomicAdd(bl.wide_queue, lane == 0 ? 1u : 0u);  // as betti_wide_body
+        const int64_t wi = (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)ticket, 0);
+        if (wi >= total) break;
+        const int64_t gi = (int64_t)(int32_t)uniw((uint32_t)bl.wide_list[wi]);
+        const int n = (int)uniw((uint32_t)bl.npoints[gi]);
+        if (n > ly.nmax) {
+            if (lane == 0) atomicOr(bl.error_flag, kEPoints);
+            if (bl.features && lane < 35) bl.features[35 * gi + lane] = __builtin_nan("");
+            if (bl.counts && lane < 4) bl.counts[4 * gi + lane] = -1;
+            continue;
+        }
+        WideCx<KW, kC16, true> cx{bl, ly, nullptr, nullptr, scr, n, (n + 63) / 64, bl.thr, 0u, 0, 0, 0, 0};
+        cx.vals = bl.rank_sorted + wi * bl.rank_stride;
+        cx.wslot = wi;
+        cx.dm = reinterpret_cast<const uint8_t*>(bl.walk.dmat + wi * bl.walk.dstride);
+        cx.mce = bl.walk.mce + wi * bl.walk.mstride;
+        cx.d0p = bl.walk.d0 + wi * bl.walk.d0stride;
+        cx.apparent(gi, wi);
+        const bool ok = cx.reduce_finish(gi, bl.weight ? bl.weight[gi] : 1.0);
+        if (ok && bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
+    }
+}
+template <int KW, bool PRE>
 __global__ __launch_bounds__(kWave * kWideWaves) __attribute__((amdgpu_waves_per_eu(DGN_WIDE_C16_WAVES)))
 void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
-    betti_wide_body<KW, kC16>(bl, ly);
+    if constexpr (PRE) betti_reduce_body<KW>(bl, ly);
+    else betti_wide_body<KW, kC16, false>(bl, ly);
+}
+
+// ---- the apparent phase as a workgroup-per-complex pass (u16-coded complexes, the 10 A path) ----
+// The per-wave wide kernel spent about 65 % of a 10 A complex in its dim-2 apparent walk (DESIGN.md
+// 3.2): every triangle's walk reads d(a, k), d(b, k), d(c, k) for its candidates k, scattered 2-byte
+// reads of a 232 KB per-wave scratch matrix, ~1.95 M vector-memory instructions per complex, bound
+// by the texture path's per-lane address rate. Here the complex's packed u16 code triangle (<= 128 KB
+// at 362 points) and its adjacency bitsets (<= 17 KB) sit in the LDS of one CU, and 16 waves run
+// every phase that needs them from there (ds_read_u16, 32 lanes per LDS cycle): the spanning forest
+// (dim 0, one wave), the dim-1 apparent pass and the dim-2 apparent walk of its ~10^6 triangles. The
+// pass writes per complex what the reductions read (betti_wide_kernel_c16<KW, true>, which then needs
+// no LDS): the full n x n code matrix (coalesced rows), the dim-0 deaths, the dim-1 min-cofacet
+// table, the dim-1 columns and the dim-2 columns not in an apparent pair with their F-minimal
+// cofacet (their initial pivot), and the triangles the dim-1 apparent pairs clear. These are exactly
+// what the per-wave kernel's own passes build (the dim-2 walk covers every triangle; the cleared ones
+// are dropped when the reduction kernel reads the list). No dim-2 min-cofacet table: the reduction
+// decides apparent owners from the matrix (lookup, PRE form).
+constexpr int kWalkWaves = 16;
+__device__ __forceinline__ uint32_t walk_ticket(uint32_t* ctr) {  // wave-uniform, no branch on the lane
+    const uint32_t t = atomicAdd(ctr, lane_id() == 0 ? 1u : 0u);
+    return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
+}
+// LDS counters of the walk pass
+enum { kWcWalk = 0, kWcN2 = 1, kWcTmax = 2, kWcRow = 3, kWcN1 = 4, kWcCl = 5, kWcD0 = 6, kWcInf0 = 7 };
+// append the lanes with `p` to a per-complex list whose length is LDS counter *ctr (one LDS atomic
+// per wave); returns this lane's slot
+__device__ __forceinline__ uint32_t walk_append(uint32_t* ctr, bool p) {
+    const uint64_t bal = ballot(p);
+    if (!bal) return 0u;
+    const uint32_t base =
+        (uint32_t)__builtin_amdgcn_readlane((int)atomicAdd(ctr, lane_id() == 0 ? (uint32_t)__popcll(bal) : 0u), 0);
+    return base + (uint32_t)mask_prefix(bal);
+}
+__global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLaunch bl) {
+    using H = WideCx<2, kC16>;  // packing helpers (9-bit vertices, keys (code << 32) | ~index)
+    extern __shared__ uint64_t walk_lds[];
+    const WalkOut& wo = bl.walk;
+    const int64_t wi = blockIdx.x;
+    if (wi >= (int64_t)*bl.wide_len) return;  // past the slice's device-side length: the whole block
+    const int lane = lane_id();
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int64_t gi = bl.wide_list[wi];
+    const int n = bl.npoints[gi];
+    const int W = (n + 63) / 64;
+    const int wmax = (wo.nmax + 63) / 64;
+    const int np4 = (wo.nmax + 3) & ~3;
+    uint64_t* adj = walk_lds;                                              // [n][W]
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(walk_lds + wo.nmax * wmax);  // kWc* counters
+    uint16_t* par = reinterpret_cast<uint16_t*>(ctr + 8);                  // forest parents, 0xFFFF = root
+    uint16_t* d0c = par + np4;                                             // dim-0 death codes
+    uint16_t* T = d0c + np4;                                               // packed codes, row i at c2(i)
+    const uint32_t* vals = bl.rank_sorted + wi * bl.rank_stride;           // code -> f32 bits
+    for (int i = threadIdx.x; i < n * W; i += kWave * kWalkWaves) adj[i] = 0ull;
+    if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
+    __syncthreads();
+    // (1) codes into LDS; adjacency d <= thr (ripser.cpp:386-395) by row ballots, mirrored bits by
+    // LDS atomics (rows are shared between waves); the threshold code = the largest code <= thr
+    {
+        const float* L = bl.lower + gi * bl.tri_stride;
+        const uint32_t* Lc = bl.rank_codes + wi * bl.rank_stride;
+        uint32_t tmax = 0;
+        for (int i = 1 + wv; i < n; i += kWalkWaves) {
+            const int ci = c2i(i);
+            for (int j0 = 0; j0 < i; j0 += kWave) {
+                const int j = j0 + lane;
+                bool e = false;
+                if (j < i) {
+                    const uint32_t code = Lc[ci + j];
+                    T[ci + j] = (uint16_t)code;
+                    e = L[ci + j] <= bl.thr;
+                    if (e) tmax = max(tmax, code);
+                }
+                const uint64_t b = ballot(e);
+                if (lane == 0 && b) atomicOr((unsigned long long*)&adj[i * W + (j0 >> 6)], b);
+                if (e) atomicOr((unsigned long long*)&adj[j * W + (i >> 6)], 1ull << (i & 63));
+            }
+        }
+        tmax = ~wave_min_u32(~tmax);
+        if (lane == 0) atomicMax(&ctr[kWcTmax], tmax);
+    }
+    __syncthreads();
+    const uint32_t thrc = ctr[kWcTmax];
+    auto aw = [&](int v, int w) __attribute__((always_inline)) { return adj[v * W + w]; };
+    // d(x, k), x != k, from the packed triangle: cx = c2(x), ck = c2(k)
+    auto dd = [&](int x, int cx, int k, int ck) __attribute__((always_inline)) -> uint32_t {
+        return T[k < x ? cx + k : ck + x];
+    };
+    // (2) the full matrix (row-major, coalesced rows) for the reductions; wave 0: dim 0, Prim on
+    // F-keys == Kruskal's forest in Ripser's order (ripser.cpp:725-762), as WideCx::prim
+    if (wv == 0) {
+        constexpr int KWM = (kC16MaxPoints + 63) / 64;
+        uint64_t best[KWM];
+        int bp[KWM];
+        uint32_t intree = lane == 0 ? 1u : 0u;  // bit t: vertex 64 t + lane is in the forest
+        for (int i = lane; i < n; i += kWave) par[i] = 0xFFFF;
+#pragma unroll
+        for (int t = 0; t < KWM; ++t) {
+            const int v = 64 * t + lane;
+            best[t] = kInfW;
+            bp[t] = 0;
+            if (t < W && v < n && v != 0 && ((aw(0, t) >> lane) & 1ull)) best[t] = H::wkey(T[c2i(v)], bin2(v));
+        }
+        // a death's value is 0 iff its code is 0 and the complex's smallest distance is 0 (codes are
+        // first indices of value runs in the sorted triangle)
+        const bool zero0 = __uint_as_float(vals[0]) == 0.0f;
+        wave_lds_order();
+        int nd0 = 0, ninf = 1;
+        for (int added = 1; added < n; ++added) {
+            uint64_t lmin = kInfW;
+            int lt = 0, lp = 0, lfree = 1 << 30;
+#pragma unroll
+            for (int t = 0; t < KWM; ++t) {
+                const int v = 64 * t + lane;
+                const bool out = t < W && v < n && !((intree >> t) & 1u);
+                if (out && best[t] < lmin) {
+                    lmin = best[t];
+                    lt = t;
+                    lp = bp[t];
+                }
+                if (out && v < lfree) lfree = v;
+            }
+            const uint64_t m = wave_min_u64(lmin);
+            int v;
+            if (m == kInfW) {  // new component: lowest vertex outside the forest
+                v = (int)wave_min_u32((uint32_t)lfree);
+                ++ninf;
+            } else {
+                const int l = __ffsll((unsigned long long)ballot(lmin == m)) - 1;
+                v = 64 * (int)rlw((uint32_t)lt, l) + l;
+                const int u = (int)rlw((uint32_t)lp, l);
+                const uint32_t dc = H::kdiam(m);
+                if (!(dc == 0u && zero0)) {  // (0, d) emitted only if d != 0 (ripser.cpp:741-748)
+                    if (lane == 0) d0c[nd0] = (uint16_t)dc;
+                    ++nd0;
+                }
+                if (lane == 0) par[v] = (uint16_t)u;
+            }
+            if (lane == (v & 63)) intree |= 1u << (v >> 6);
+            wave_lds_order();
+            const int cv = c2i(v);
+#pragma unroll
+            for (int t = 0; t < KWM; ++t) {
+                const int x = 64 * t + lane;
+                if (t < W && x < n && !((intree >> t) & 1u) && ((aw(v, t) >> lane) & 1ull)) {
+                    const uint64_t k = H::wkey(dd(v, cv, x, c2i(x)), v > x ? bin2(v) + x : bin2(x) + v);
+                    if (k < best[t]) {
+                        best[t] = k;
+                        bp[t] = v;
+                    }
+                }
+            }
+        }
+        wave_lds_order();
+        float* d0s = wo.d0 + wi * wo.d0stride;
+        for (int i = lane; i < nd0; i += kWave) d0s[i] = __uint_as_float(vals[d0c[i]]);
+        if (lane == 0) {
+            ctr[kWcD0] = (uint32_t)nd0;
+            ctr[kWcInf0] = (uint32_t)ninf;
+        }
+    } else {
+        uint16_t* D = wo.dmat + wi * wo.dstride;
+        for (int i = wv - 1; i < n; i += kWalkWaves - 1) {
+            const int ci = c2i(i);
+            for (int x = lane; x < n; x += kWave)
+                D[i * n + x] = x == i ? (uint16_t)0xFFFF : (x < i ? T[ci + x] : T[c2i(x) + i]);
+        }
+    }
+    __syncthreads();  // the forest (is a dim-1 column a tree edge?)
+    // (3) dim 1, one lane per edge (i, j), j < i, rows dealt from an LDS cursor (WideCx::pass_dim1):
+    // the F-minimal cofacet of every non-tree edge (walking k downwards, the first k with both
+    // distances within d(i, j) ends the walk; a smaller k wins only with a strictly smaller
+    // diameter), the min-cofacet table, the apparent pairs' triangles (cleared in dim 2) and the
+    // other columns
+    {
+        uint16_t* mce = wo.mce + wi * wo.mstride;
+        uint64_t* oe1 = wo.e1 + wi * (int64_t)wo.cap1;
+        uint32_t* ocl = wo.cl + wi * (int64_t)wo.cap1;
+        for (;;) {
+            const int i = 1 + (int)walk_ticket(&ctr[kWcRow]);
+            if (i >= n) break;
+            const int ci = c2i(i);
+            for (int w0 = 0; 64 * w0 < i; ++w0) {
+                uint64_t bits = uniw64(aw(i, w0));
+                const int lim = i - 64 * w0;
+                if (lim < 64) bits &= (1ull << lim) - 1ull;
+                if (!bits) continue;
+                const int j = 64 * w0 + lane;
+                bool app = false, na = false;
+                uint32_t clr = 0;
+                uint64_t ent = 0;
+                if ((bits >> lane) & 1ull) {
+                    uint16_t mc = kMcNoneW;
+                    if (!(par[i] == j || par[j] == i)) {
+                        const uint32_t dij = T[ci + j];
+                        const int cj = c2i(j);
+                        int bk = -1;
+                        bool found = false;
+                        uint32_t bdd = 0xFFFFFFFFu, hda = 0, hdb = 0;
+                        for (int w = W - 1; w >= 0 && !found; --w) {
+                            uint64_t m = aw(i, w) & aw(j, w);
+                            while (m != 0ull && !found) {
+                                const int bit = 63 - __clzll((long long)m);
+                                m &= ~(1ull << bit);
+                                const int k = 64 * w + bit;
+                                const int ck = c2i(k);
+                                const uint32_t da = dd(i, ci, k, ck), db = dd(j, cj, k, ck);
+                                const uint32_t dk = max(da, db);
+                                if (dk <= dij) {
+                                    bdd = dij;
+                                    bk = k;
+                                    found = true;
+                                    hda = da;
+                                    hdb = db;
+                                } else if (dk < bdd) {
+                                    bdd = dk;
+                                    bk = k;
+                                }
+                            }
+                        }
+                        if (bk >= 0) {
+                            const uint32_t ed = ((uint32_t)i << 9) | (uint32_t)j;
+                            app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
+                            if (app) clr = (uint32_t)H::pidx(3, H::pinsert(2, ed, bk));
+                            else {
+                                na = true;
+                                ent = (uint64_t)ed | ((uint64_t)bk << 18) | ((uint64_t)bdd << 27);
+                            }
+                            mc = (uint16_t)bk;
+                        }
+                    }
+                    mce[ci + j] = mc;
+                }
+                const uint32_t q1 = walk_append(&ctr[kWcN1], na);
+                if (na && q1 < (uint32_t)wo.cap1) oe1[q1] = ent;
+                const uint32_t q2 = walk_append(&ctr[kWcCl], app);
+                if (app && q2 < (uint32_t)wo.cap1) ocl[q2] = clr;
+            }
+        }
+    }
+    // (4) the dim-2 walk. Each wave takes top vertices a (descending: the largest share of triangles
+    // first) from an LDS cursor and deals the triangles (a, b, c), c < b < a, of a's edges to its
+    // lanes as the per-wave kernel's pass_dim2 does from its edge list; a lane whose walk ended
+    // takes the next triangle at once.
+    uint64_t* oent = wo.ent + wi * (int64_t)wo.cap;
+    int ca = -1, cb = 0, cw = 0, bw = 0;  // cursor (uniform): edge (ca, cb), word cw of its c's
+    uint64_t cm = 0, bm = 0;              // c's of word cw not yet dealt; b's of row ca word bw not yet taken
+    bool exhausted = false;
+    int ea = 0, eb = 0, c = 0, w = 0, bk = -1;
+    int ra = 0, rb = 0, rcc = 0;  // c2 of the lane's triangle's vertices
+    bool act = false, fresh = false, found = false;
+    uint64_t m = 0;
+    uint32_t bd = 0xFFFFFFFFu, ds = 0, dab = 0, dac = 0, dbc = 0, hda = 0, hdb = 0, hdc = 0;
+    for (;;) {
+        for (;;) {  // lanes without a triangle take the next ones, in order
+            const uint64_t need = ballot(!act);
+            if (!need) break;
+            while (cm == 0ull && !exhausted) {
+                if (ca >= 0 && cb > 0 && 64 * (cw + 1) < cb) {
+                    ++cw;
+                } else {
+                    while (bm == 0ull) {  // the next b of row ca, or the next top vertex
+                        if (ca >= 0 && 64 * (bw + 1) < ca) {
+                            ++bw;
+                        } else {
+                            ca = n - 1 - (int)walk_ticket(&ctr[kWcWalk]);
+                            if (ca < 2) {
+                                exhausted = true;
+                                break;
+                            }
+                            bw = 0;
+                        }
+                        uint64_t r = uniw64(aw(ca, bw));
+                        const int lim = ca - 64 * bw;
+                        if (lim < 64) r &= (1ull << lim) - 1ull;
+                        bm = r;
+                    }
+                    if (exhausted) break;
+                    cb = 64 * bw + __ffsll((unsigned long long)bm) - 1;
+                    bm &= bm - 1ull;
+                    cw = 0;
+                }
+                uint64_t mm = uniw64(aw(ca, cw) & aw(cb, cw));
+                const int lim = cb - 64 * cw;
+                if (lim < 64) mm &= (1ull << lim) - 1ull;
+                cm = mm;
+            }
+            if (cm == 0ull) break;  // every triangle dealt
+            const int p = __popcll(cm), q = __popcll(need);
+            const int r = mask_prefix(need);
+            if (!act && r < p) {
+                c = 64 * cw + H::select_bit(cm, r);
+                ea = ca;
+                eb = cb;
+                act = fresh = true;
+            }
+            cm = q >= p ? 0ull : cm & ~((1ull << H::select_bit(cm, q)) - 1ull);
+        }
+        if (!ballot(act)) break;
+        bool na = false;
+        uint64_t ent = 0;
+        if (act) {
+            if (fresh) {
+                ra = c2i(ea);
+                rb = c2i(eb);
+                rcc = c2i(c);
+                dab = T[ra + eb];
+                dac = T[ra + c];
+                dbc = T[rb + c];
+                ds = max(max(dab, dac), dbc);
+                w = W - 1;
+                m = aw(ea, w) & aw(eb, w) & aw(c, w);
+                bd = 0xFFFFFFFFu;
+                bk = -1;
+                found = false;
+                fresh = false;
+            }
+            constexpr int kS = 4;  // candidates per step, highest first
+            int kk[kS];
+            bool val[kS];
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+                while (m == 0ull && w > 0) {
+                    --w;
+                    m = aw(ea, w) & aw(eb, w) & aw(c, w);
+                }
+                val[j] = m != 0ull;
+                const int bit = val[j] ? 63 - __clzll((long long)m) : 0;
+                kk[j] = 64 * w + bit;
+                if (val[j]) m &= ~(1ull << bit);
+            }
+            uint32_t da[kS], dbv[kS], dc[kS];
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+                const int k = val[j] ? kk[j] : c;  // d(c, c): a harmless in-range read
+                const int ck = c2i(k);
+                da[j] = dd(ea, ra, k, ck);
+                dbv[j] = dd(eb, rb, k, ck);
+                dc[j] = dd(c, rcc, k, ck);
+            }
+            // (diameter, k) only: walking k downwards a smaller k wins only with a strictly smaller
+            // diameter (pass_dim2)
+#pragma unroll
+            for (int j = 0; j < kS; ++j) {
+                if (!val[j] || found) continue;
+                const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
+                if (dk <= ds) {
+                    bd = ds;
+                    bk = kk[j];
+                    found = true;
+                    hda = da[j];
+                    hdb = dbv[j];
+                    hdc = dc[j];
+                } else if (dk < bd) {
+                    bd = dk;
+                    bk = kk[j];
+                }
+            }
+            if (found || !val[kS - 1]) {
+                act = false;
+                if (bk >= 0) {
+                    const uint32_t colp = ((uint32_t)ea << 18) | ((uint32_t)eb << 9) | (uint32_t)c;
+                    const bool app = found && (bk > ea || max(max(hdb, hdc), dbc) < ds) &&
+                                     (bk > eb || max(max(hda, hdc), dac) < ds) &&
+                                     (bk > c || max(max(hda, hdb), dab) < ds);
+                    if (!app) {  // the column, its cofacet vertex, the cofacet's diameter (WalkOut::ent)
+                        na = true;
+                        ent = (uint64_t)colp | ((uint64_t)bk << 27) | ((uint64_t)bd << 36);
+                    }
+                }
+            }
+        }
+        const uint32_t q = walk_append(&ctr[kWcN2], na);
+        if (na && q < (uint32_t)wo.cap) oent[q] = ent;
+    }
+    (void)thrc;
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const int t = threadIdx.x;
+        const uint32_t v = t == kWmNa2 ? ctr[kWcN2] : t == kWmThr ? thrc : t == kWmNa1 ? ctr[kWcN1]
+                         : t == kWmCl ? ctr[kWcCl] : t == kWmD0 ? ctr[kWcD0] : t == kWmInf0 ? ctr[kWcInf0] : 0u;
+        wo.meta[8 * wi + t] = v;
+    }
+}
+
+size_t walk_lds_bytes(int nmax) {
+    const int64_t wmax = (nmax + 63) / 64, np4 = (nmax + 3) & ~3;
+    return (size_t)(8 * nmax * wmax + 32 + 2 * 2 * np4 + 2 * ((int64_t)nmax * (nmax - 1) / 2) + 8);
 }
 
 int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }
 
 // the instantiation for complexes of up to nmax points: 2, 4, 6 or 8 bitset words per vertex
 using WideKernel = void (*)(BettiLaunch, WideLayout);
-WideKernel wide_kernel_for(int nmax, bool c16) {
+WideKernel wide_kernel_for(int nmax, bool c16, bool pre = false) {
     const int w = (nmax + 63) / 64;
     if (c16 && nmax <= kC16MaxPoints) {  // u16 rank codes (betti_rank_codes before the launch)
-        if (w <= 2) return betti_wide_kernel_c16<2>;
-        if (w <= 4) return betti_wide_kernel_c16<4>;
-        return betti_wide_kernel_c16<6>;
+        if (pre) {  // after the walk pass (betti_walk_kernel)
+            if (w <= 2) return betti_wide_kernel_c16<2, true>;
+            if (w <= 4) return betti_wide_kernel_c16<4, true>;
+            return betti_wide_kernel_c16<6, true>;
+        }
+        if (w <= 2) return betti_wide_kernel_c16<2, false>;
+        if (w <= 4) return betti_wide_kernel_c16<4, false>;
+        return betti_wide_kernel_c16<6, false>;
     }
     if (w <= 2) return betti_wide_kernel<2, kF32>;
     if (w <= 4) return betti_wide_kernel<4, kF32>;
@@ -1203,7 +1772,8 @@ WideKernel wide_kernel_for(int nmax, bool c16) {
     return betti_wide_kernel<32, kHuge>;              // 1025..2048 points: HUGE
 }
 
-size_t wide_lds_bytes(int nmax) {  // per workgroup: token, adjacency, parents
+size_t wide_lds_bytes(int nmax, bool pre = false) {  // per workgroup: token, adjacency, parents
+    if (pre) return 0;  // the reduction-only launch after the walk pass
     const int64_t ww = (nmax + 63) / 64;
     if (nmax > kWideBigPoints) return (size_t)(8 * (1 + (nmax + 3) / 4));  // parents only
     return (size_t)(8 * (1 + nmax * ww + (nmax + 3) / 4));
@@ -1218,7 +1788,7 @@ size_t wide_lds_bytes(int nmax) {  // per workgroup: token, adjacency, parents
 // entries. The host raises `grow` while complexes still overflow (kWideMaxGrow levels): a complex
 // outgrows the last level only when it needs more than kWideMaxCols (2^29) columns, pivots or pairs
 // or a V store above 2^(base_log2 + 6) entries.
-WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, int base_log2) {
+WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, int base_log2, bool prewalked) {
     WideLayout l{};
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
@@ -1247,10 +1817,12 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
         o = align256(o + bytes);
         return at;
     };
-    l.D = take(4 * n * n);
-    l.mc_e = take(2 * e);
-    l.mc_t = take(2 * t);
-    l.edges = take(4 * e);
+    l.prewalked = prewalked ? 1 : 0;
+    l.D = take(prewalked ? 0 : 4 * n * n);  // prewalked: the walk pass's per-complex matrix
+    l.mc_e = take(prewalked ? 0 : 2 * e);   // prewalked: the walk pass's per-complex table
+    l.mc_t = take(prewalked ? 0 : 2 * t);   // prewalked: no dim-2 min-cofacet table
+    l.clb = take(prewalked ? 4 * (t / 32 + 2) : 0);
+    l.edges = take(prewalked ? 0 : 4 * e);
     l.adj = take(huge ? 8 * n * ((n + 63) / 64) : 0);
     l.na_key = take(8 * cap);
     l.na_tau = take(8 * cap);
@@ -1264,7 +1836,7 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
     l.h_used = take(4 * cap);
     l.p1 = take(8 * cap);
     l.p2 = take(8 * cap);
-    l.d0 = take(4 * n);
+    l.d0 = take(prewalked ? 0 : 4 * n);
     l.total = o;
     return l;
 }
@@ -1272,29 +1844,52 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
 hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves) {
     hipError_t e = hipMemset2DAsync(l.base + l.h_key, (size_t)l.total, 0, 8 * (size_t)l.h_cap, (size_t)waves, s);
     if (e != hipSuccess) return e;
-    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.edges
-    return hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.edges - l.mc_e), (size_t)waves, s);
+    // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.clb
+    if (l.clb > l.mc_e) e = hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.clb - l.mc_e), (size_t)waves, s);
+    if (e != hipSuccess || !l.prewalked) return e;
+    return hipMemset2DAsync(l.base + l.clb, (size_t)l.total, 0, (size_t)(l.edges - l.clb), (size_t)waves, s);
 }
 
 // waves of betti_wide_kernel resident on the whole device for complexes of up to nmax points
-int betti_wide_resident_waves(int device, int nmax, bool c16) {
+int betti_wide_resident_waves(int device, int nmax, bool c16, bool pre) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 512;
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, c16), kWave * kWideWaves,
-                                                     wide_lds_bytes(nmax)) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, wide_kernel_for(nmax, c16, pre), kWave * kWideWaves,
+                                                     wide_lds_bytes(nmax, pre)) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
     return prop.multiProcessorCount * per_cu * kWideWaves;
+}
+
+WalkOut betti_walk_out_layout(int nmax) {
+    WalkOut w{};
+    w.nmax = nmax;
+    w.dstride = ((int64_t)nmax * nmax + 127) / 128 * 128;          // u16
+    w.d0stride = ((int64_t)nmax + 63) / 64 * 64;                   // f32
+    w.mstride = ((int64_t)nmax * (nmax - 1) / 2 + 127) / 128 * 128;  // u16
+    w.cap1 = kWalkCap;
+    w.cap = kWalkCap;
+    return w;
+}
+int64_t betti_walk_out_bytes(int nmax) {
+    const WalkOut w = betti_walk_out_layout(nmax);
+    return 2 * w.dstride + 32 + 4 * w.d0stride + 2 * w.mstride + (8 + 4) * (int64_t)w.cap1 + 8 * (int64_t)w.cap;
+}
+hipError_t launch_betti_walk(hipStream_t st, const BettiLaunch& b, int64_t count, int nmax) {
+    if (count <= 0) return hipSuccess;
+    if (nmax > kC16MaxPoints || nmax < 3) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(betti_walk_kernel, dim3((unsigned)count), dim3(kWave * kWalkWaves), walk_lds_bytes(nmax), st, b);
+    return hipGetLastError();
 }
 
 hipError_t launch_betti_wide(hipStream_t st, const BettiLaunch& b, const WideLayout& l, int waves) {
     if (waves <= 0) return hipSuccess;
     WideLayout lw = l;
     lw.slots = waves;  // scratch slots allocated: a wave past them leaves at once
-    hipLaunchKernelGGL(wide_kernel_for(l.nmax, b.rank_codes != nullptr && l.nmax <= kC16MaxPoints),
+    hipLaunchKernelGGL(wide_kernel_for(l.nmax, b.rank_codes != nullptr && l.nmax <= kC16MaxPoints, l.prewalked != 0),
                        dim3((unsigned)((waves + kWideWaves - 1) / kWideWaves)), dim3(kWave * kWideWaves),
-                       wide_lds_bytes(l.nmax), st, b, lw);
+                       wide_lds_bytes(l.nmax, l.prewalked != 0), st, b, lw);
     return hipGetLastError();
 }
 

@@ -135,7 +135,7 @@ struct dgn_ctx {
     int64_t host_syncs = 0;           // host waits on the stream (dgn_debug_host_syncs)
     // betti workspace
     DevBuf b_scratch, b_list, b_lower, b_np, b_w, b_wlist, b_wide, b_rlist, b_rlist2, b_big, b_rank, b_rscal, b_rank16,
-        b_rscal16;
+        b_rscal16, b_walk;
     int betti_slots = 0;
     bool scratch_fresh = false;  // b_scratch (re)allocated: min-cofacet tables need initialising
     // overflow-tier fork (side stream + events), created on first use
@@ -143,11 +143,14 @@ struct dgn_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int cus = 0;  // compute units of the device (device_cus)
     int wide_nmax = 0, wide_waves = 0, wide_cap = 0;  // layout the wide scratch's tables were initialised for
+    int wide_pre = -1;
     // debug / A-B knobs (dgn_ctx_set_debug; never read from the environment)
     bool dbg_force_retry = false;  // every complex of a Betti pass through the capacity-retry launch
     int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
     int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
+    bool dbg_wide_walk = true;     // the u16-coded complexes' dim-2 walk as a workgroup-per-complex pass
+    int dbg_split_chunk = 0;       // clouds per chunk of the component split (0 = its byte budget)
     int dbg_big_log2 = 0;          // capacity-retry layout's first-level table size log2 (0 = natural 24)
     int dbg_emit_chunk = 0;        // tiles per launch of the large-row emit (0 = the byte budget's)
     // host staging
@@ -489,9 +492,13 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
     // (distance matrix, min-cofacet tables, sorted columns, pivot hash) sized for max_points
     WideLayout wl{};
     int wide_waves = 0;
+    // wide complexes of <= kC16MaxPoints points run on u16 rank codes, and their dim-2 apparent walk
+    // runs as a workgroup-per-complex pass before the per-wave launch (betti_walk_kernel)
+    const bool c16 = c->dbg_wide_c16 && max_points > 64 && max_points <= kC16MaxPoints;
+    const bool prewalk = c16 && c->dbg_wide_walk;
     if (max_points > 64) {
         const int wide_nmax = std::min(max_points, kWideRegular);  // larger: the coded retry launch
-        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap);
+        wl = betti_wide_layout(wide_nmax, false, c->dbg_wide_cap, 0, 24, prewalk);
         // as many waves as the device keeps resident (dynamic LDS sized by
         // max_points), each with its own scratch, within half of the HBM that is free or already
         // this workspace's (288 GB per MI355X; at least 8 GB) -- counting the workspace in the pool
@@ -501,15 +508,15 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const int64_t budget =
             std::max<int64_t>(int64_t(8) << 30, ((int64_t)free_b + (int64_t)c->b_wide.bytes) / 2);
-        const int64_t resident =
-            betti_wide_resident_waves(c->device, wide_nmax, c->dbg_wide_c16 && wide_nmax <= kC16MaxPoints);
+        const int64_t resident = betti_wide_resident_waves(c->device, wide_nmax, c16, prewalk);
         wide_waves = (int)std::max<int64_t>(1, std::min<int64_t>({budget / wl.total, resident, A}));
         if (c->dbg_wide_waves > 0 && c->dbg_wide_waves < wide_waves) wide_waves = c->dbg_wide_waves;  // A/B only
         const size_t want = (size_t)wl.total * (size_t)wide_waves;
         const bool grown = c->b_wide.bytes < want;
         if (grown) HIP_TRY(c, c->b_wide.ensure(want));
         wl.base = c->b_wide.as<uint8_t>();
-        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap) {
+        if (grown || c->wide_nmax != wide_nmax || c->wide_waves != wide_waves || c->wide_cap != wl.na_cap ||
+            c->wide_pre != (int)prewalk) {
             // the layout depends on max_points: every wave's pivot hash table starts empty (key 0)
             // and its u16 min-cofacet tables "no cofacet" (0xFFFF); afterwards each reduction
             // restores both for the entries it used
@@ -517,6 +524,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             c->wide_nmax = wide_nmax;
             c->wide_waves = wide_waves;
             c->wide_cap = wl.na_cap;
+            c->wide_pre = (int)prewalk;
         }
         HIP_TRY(c, c->b_wlist.ensure(sizeof(int32_t) * (size_t)A));
     }
@@ -565,7 +573,6 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         // wide complexes of <= 362 points run on u16 rank codes (half the per-wave distance matrix
         // the scattered walk and pivot-search reads miss on): the narrow launches and the bucket
         // pass first, then per slice of the wide list its codes (betti_rank_codes) and a wide launch
-        const bool c16 = c->dbg_wide_c16 && max_points > 64 && max_points <= kC16MaxPoints;
         {
             TimedLaunch t(c, "betti_vr", bytes, 0.0);
             HIP_TRY(c, launch_betti(c->stream, pb, max_points, c->betti_slots,
@@ -578,8 +585,22 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                 const int64_t nwide = given ? cnt : std::min<int64_t>(cnt, nw().wide_atoms);
                 if (nwide > 0) {
                     const int64_t rstride = ((int64_t)max_points * (max_points - 1) / 2 + 63) / 64 * 64;
-                    const int64_t slice = std::max<int64_t>(
+                    int64_t slice = std::max<int64_t>(
                         1, std::min<int64_t>({nwide, (int64_t(16) << 30) / (20 * rstride), INT32_MAX / rstride}));
+                    // the walk pass's per-complex outputs (matrix, bitsets, dim-2 column list: ~2 MB at
+                    // 340 points) within a quarter of the HBM that is free or already theirs, <= 32 GB
+                    const int64_t walk_bytes = prewalk ? betti_walk_out_bytes(max_points) : 0;
+                    if (prewalk) {
+                        size_t free_b = 0, total_b = 0;
+                        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+                        const int64_t wbudget = std::min<int64_t>(
+                            int64_t(32) << 30, std::max<int64_t>(int64_t(1) << 30, ((int64_t)free_b + (int64_t)c->b_walk.bytes) / 4));
+                        slice = std::max<int64_t>(1, std::min<int64_t>(slice, wbudget / walk_bytes));
+                    }
+                    // equal slices: a short last slice leaves its launch's resident waves idle behind
+                    // a tail of single complexes
+                    slice = (nwide + (nwide + slice - 1) / slice - 1) / ((nwide + slice - 1) / slice);
+                    if (prewalk) HIP_TRY(c, c->b_walk.ensure((size_t)walk_bytes * (size_t)slice));
                     const size_t tmp_bytes = betti_rank_temp_bytes(slice, rstride);
                     HIP_TRY(c, c->b_rank16.ensure(8 * (size_t)slice * rstride + tmp_bytes));
                     const int64_t nsl = (nwide + slice - 1) / slice;
@@ -600,6 +621,24 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                         wb.rank_codes = codes;
                         wb.rank_sorted = sorted;
                         wb.rank_stride = rstride;
+                        if (prewalk) {
+                            WalkOut wo = betti_walk_out_layout(max_points);
+                            uint8_t* p = c->b_walk.as<uint8_t>();
+                            auto carve = [&](int64_t bytes_per_complex) {
+                                uint8_t* q = p;
+                                p += (size_t)bytes_per_complex * (size_t)slice;
+                                return q;
+                            };
+                            wo.dmat = reinterpret_cast<uint16_t*>(carve(2 * wo.dstride));
+                            wo.meta = reinterpret_cast<uint32_t*>(carve(32));
+                            wo.d0 = reinterpret_cast<float*>(carve(4 * wo.d0stride));
+                            wo.mce = reinterpret_cast<uint16_t*>(carve(2 * wo.mstride));
+                            wo.e1 = reinterpret_cast<uint64_t*>(carve(8 * (int64_t)wo.cap1));
+                            wo.cl = reinterpret_cast<uint32_t*>(carve(4 * (int64_t)wo.cap1));
+                            wo.ent = reinterpret_cast<uint64_t*>(carve(8 * (int64_t)wo.cap));
+                            wb.walk = wo;
+                            HIP_TRY(c, launch_betti_walk(c->stream, wb, ub, max_points));
+                        }
                         HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, ub)));
                     }
                 }
@@ -916,6 +955,8 @@ int dgn_ctx_set_debug(dgn_ctx* c, int knob, int value) {
         case DGN_DEBUG_FORCE_RETRY: c->dbg_force_retry = value != 0; return DGN_OK;
         case DGN_DEBUG_WIDE_WAVES: c->dbg_wide_waves = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_WIDE_C16: c->dbg_wide_c16 = value != 0; return DGN_OK;
+        case DGN_DEBUG_WIDE_WALK: c->dbg_wide_walk = value != 0; return DGN_OK;
+        case DGN_DEBUG_SPLIT_CHUNK: c->dbg_split_chunk = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_WIDE_CAP: c->dbg_wide_cap = value > 0 ? value : 0; return DGN_OK;
         case DGN_DEBUG_BIG_LOG2: c->dbg_big_log2 = value > 0 && value < 24 ? value : 0; return DGN_OK;
         case DGN_DEBUG_EMIT_CHUNK: c->dbg_emit_chunk = value > 0 ? value : 0; return DGN_OK;
@@ -1316,7 +1357,8 @@ static int persistence_split(dgn_ctx* c, const double* d_clouds, const float* d_
                              int32_t cap, std::vector<int32_t>& kk) {
     const int64_t tri_in = (int64_t)max_points * (max_points - 1) / 2;  // caller-given packing
     const int64_t tri_stride = (tri_in + 3) / 4 * 4;
-    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(C, (int64_t(8) << 30) / (4 * tri_stride)));
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(C, (int64_t(8) << 30) / (4 * tri_stride)));
+    if (c->dbg_split_chunk > 0) chunk = std::min<int64_t>(chunk, c->dbg_split_chunk);  // tests only
     DevBuf tri, lab, dmap, doff, dsize, dsrc, sub, snp, spairs, scnt;
     if (d_clouds) HIP_TRY(c, tri.ensure(4 * (size_t)(chunk * tri_stride)));
     HIP_TRY(c, lab.ensure(4 * (size_t)(chunk * max_points)));
@@ -1366,45 +1408,74 @@ static int persistence_split(dgn_ctx* c, const double* d_clouds, const float* d_
         }
         const int64_t nsub = (int64_t)size.size();
         if (nsub == 0) continue;
-        const int64_t sub_stride = (int64_t)smax * (smax - 1) / 2;
+        (void)smax;
+        // Components in groups of similar size (largest first), each group one Betti pass whose
+        // triangle stride and pair capacity are its largest member's -- not the chunk's: a cloud with
+        // one 2,000-point cluster and thousands of 2-point components would otherwise give every
+        // component a 2,000-point triangle and a full pair block -- and whose sub-triangles and pairs
+        // stay within a byte budget
+        std::vector<int64_t> order((size_t)nsub);
+        for (int64_t q = 0; q < nsub; ++q) order[(size_t)q] = q;
+        std::stable_sort(order.begin(), order.end(),
+                         [&](int64_t x, int64_t y) { return size[(size_t)x] > size[(size_t)y]; });
         hipError_t e;
-        if ((e = dmap.ensure(4 * map.size())) || (e = doff.ensure(8 * off.size())) || (e = dsize.ensure(4 * size.size())) ||
-            (e = dsrc.ensure(4 * src.size())) || (e = sub.ensure(4 * (size_t)std::max<int64_t>(nsub * sub_stride, 1))) ||
-            (e = snp.ensure(4 * (size_t)nsub)) || (e = spairs.ensure(8 * 3 * (size_t)nsub * cap)) ||
-            (e = scnt.ensure(16 * (size_t)nsub)))
+        if ((e = dmap.ensure(4 * map.size())))
             return hip_fail(c, e, "dgn_host_persistence: component split allocation");
         HIP_TRY(c, hipMemcpyAsync(dmap.p, map.data(), 4 * map.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(doff.p, off.data(), 8 * off.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(dsize.p, size.data(), 4 * size.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(dsrc.p, src.data(), 4 * src.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(snp.p, size.data(), 4 * size.size(), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, launch_gather_sub(c->stream, T, ts, dsrc.as<int32_t>(), doff.as<int64_t>(), dsize.as<int32_t>(),
-                                     dmap.as<int32_t>(), nsub, sub.as<float>(), sub_stride));
-        int st = betti_impl(c, nullptr, threshold, nullptr, scnt.as<int32_t>(), nullptr, snp.as<int32_t>(), smax, nsub,
-                            spairs.as<float>(), cap, sub.as<float>());
-        if (st) return st;
-        std::vector<int32_t> sk(4 * (size_t)nsub);
-        std::vector<float> sp(2 * 3 * (size_t)nsub * cap);
-        HIP_TRY(c, hipMemcpy(sk.data(), scnt.p, 16 * (size_t)nsub, hipMemcpyDeviceToHost));
-        HIP_TRY(c, hipMemcpy(sp.data(), spairs.p, 8 * 3 * (size_t)nsub * cap, hipMemcpyDeviceToHost));
-        // the union of the components' pairs (counts past cap are reported by the caller)
-        for (int64_t q = 0; q < nsub; ++q) {
-            const int64_t i = c0 + src[(size_t)q];
-            int32_t* k = kk.data() + 4 * i;
-            k[1] += sk[4 * (size_t)q + 1];
-            const int col[3] = {0, 2, 3};
-            for (int d = 0; d < 3; ++d) {
-                const int32_t m = sk[4 * (size_t)q + col[d]];
-                for (int32_t t = 0; t < m && t < cap; ++t) {
-                    const int32_t slot = k[col[d]] + t;
-                    if (slot >= cap) break;
-                    const float* from = sp.data() + ((size_t)(q * 3 + d) * cap + t) * 2;
-                    float* to = pairs + ((size_t)(i * 3 + d) * cap + slot) * 2;
-                    to[0] = from[0];
-                    to[1] = from[1];
-                }
-                k[col[d]] += m;
+        constexpr int64_t kGroupBytes = int64_t(2) << 30;
+        for (int64_t g0 = 0; g0 < nsub;) {
+            const int32_t gmax = size[(size_t)order[(size_t)g0]];
+            const int64_t gstride = std::max<int64_t>(1, (int64_t)gmax * (gmax - 1) / 2);
+            // pairs per diagram of a gmax-point complex: dim 0 < gmax, dim 1 < C(gmax, 2), dim 2 < C(gmax, 3)
+            const int64_t c3 = (int64_t)gmax * (gmax - 1) * (gmax - 2) / 6;
+            const int32_t gcap = (int32_t)std::min<int64_t>(cap, std::max<int64_t>({(int64_t)gmax, gstride, c3, 1}));
+            const int64_t per = 4 * gstride + 24 * (int64_t)gcap + 64;
+            const int64_t gn = std::max<int64_t>(1, std::min<int64_t>(nsub - g0, kGroupBytes / per));
+            std::vector<int64_t> goff((size_t)gn);
+            std::vector<int32_t> gsize((size_t)gn), gsrc((size_t)gn);
+            for (int64_t t = 0; t < gn; ++t) {
+                const int64_t q = order[(size_t)(g0 + t)];
+                goff[(size_t)t] = off[(size_t)q];
+                gsize[(size_t)t] = size[(size_t)q];
+                gsrc[(size_t)t] = src[(size_t)q];
             }
+            if ((e = doff.ensure(8 * (size_t)gn)) || (e = dsize.ensure(4 * (size_t)gn)) || (e = dsrc.ensure(4 * (size_t)gn)) ||
+                (e = sub.ensure(4 * (size_t)(gn * gstride))) || (e = snp.ensure(4 * (size_t)gn)) ||
+                (e = spairs.ensure(8 * 3 * (size_t)gn * gcap)) || (e = scnt.ensure(16 * (size_t)gn)))
+                return hip_fail(c, e, "dgn_host_persistence: component split allocation");
+            HIP_TRY(c, hipMemcpyAsync(doff.p, goff.data(), 8 * (size_t)gn, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(dsize.p, gsize.data(), 4 * (size_t)gn, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(dsrc.p, gsrc.data(), 4 * (size_t)gn, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(snp.p, gsize.data(), 4 * (size_t)gn, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, launch_gather_sub(c->stream, T, ts, dsrc.as<int32_t>(), doff.as<int64_t>(), dsize.as<int32_t>(),
+                                         dmap.as<int32_t>(), gn, sub.as<float>(), gstride));
+            int st = betti_impl(c, nullptr, threshold, nullptr, scnt.as<int32_t>(), nullptr, snp.as<int32_t>(),
+                                std::max<int32_t>(gmax, 2), gn, spairs.as<float>(), gcap, sub.as<float>());
+            if (st) return st;
+            std::vector<int32_t> sk(4 * (size_t)gn);
+            std::vector<float> sp(2 * 3 * (size_t)gn * gcap);
+            HIP_TRY(c, hipMemcpy(sk.data(), scnt.p, 16 * (size_t)gn, hipMemcpyDeviceToHost));
+            HIP_TRY(c, hipMemcpy(sp.data(), spairs.p, 8 * 3 * (size_t)gn * gcap, hipMemcpyDeviceToHost));
+            // the union of the components' pairs (counts past cap are reported by the caller)
+            for (int64_t t = 0; t < gn; ++t) {
+                const int64_t i = c0 + gsrc[(size_t)t];
+                int32_t* k = kk.data() + 4 * i;
+                k[1] += sk[4 * (size_t)t + 1];
+                const int col[3] = {0, 2, 3};
+                for (int d = 0; d < 3; ++d) {
+                    const int32_t m = sk[4 * (size_t)t + col[d]];
+                    for (int32_t u = 0; u < m && u < gcap; ++u) {
+                        const int32_t slot = k[col[d]] + u;
+                        if (slot >= cap) break;
+                        const float* from = sp.data() + ((size_t)(t * 3 + d) * gcap + u) * 2;
+                        float* to = pairs + ((size_t)(i * 3 + d) * cap + slot) * 2;
+                        to[0] = from[0];
+                        to[1] = from[1];
+                    }
+                    k[col[d]] += m;
+                }
+            }
+            g0 += gn;
         }
     }
     return DGN_OK;

@@ -98,6 +98,27 @@ inline int graph_tile_atoms(int64_t num_atoms, int cus) {
 int graph_emit_cap(uint32_t max_candidates, uint64_t kmax);  // LDS cap, or kEmitGlobalKeys
 
 // ---- Betti ----
+// Outputs of the workgroup-per-complex apparent pass (betti_walk_kernel, betti_wide.hip) for the
+// u16-coded wide complexes (65..kC16MaxPoints points, the reference's 10 A default), per position
+// wi of a wide-list slice; the per-wave wide kernel then only reduces (meta == null: the per-wave
+// kernel runs the whole complex itself)
+enum { kWmNa2 = 0, kWmThr = 1, kWmNa1 = 2, kWmCl = 3, kWmD0 = 4, kWmInf0 = 5 };  // WalkOut::meta words
+struct WalkOut {
+    uint16_t* dmat;     // [slice][dstride]: the complex's full n x n u16 code matrix, diagonal 0xFFFF
+    uint32_t* meta;     // [slice][8]: kWm* (list lengths may exceed their caps: capacity retry)
+    float* d0;          // [slice][d0stride]: dim-0 deaths != 0, in Prim's order
+    uint16_t* mce;      // [slice][mstride]: dim-1 min-cofacet vertex per edge (packed index), 0xFFFF none
+    // [slice][cap1] dim-1 columns not in an apparent pair: packed edge (18 bits) | cofacet vertex << 18
+    // | cofacet diameter code << 27
+    uint64_t* e1;
+    uint32_t* cl;       // [slice][cap1] triangles cleared by the dim-1 apparent pairs (combinatorial index)
+    // [slice][cap] dim-2 columns not in an apparent pair, with their F-minimal cofacet (initial
+    // pivot): packed triangle (27 bits) | cofacet vertex << 27 | cofacet diameter code << 36
+    uint64_t* ent;
+    int64_t dstride, d0stride, mstride;
+    int32_t cap1, cap;  // powers of two
+    int32_t nmax;
+};
 struct BettiLaunch {
     int64_t num_atoms;        // complexes of this launch
     float thr;                // (float) r_cutoff
@@ -150,6 +171,7 @@ struct BettiLaunch {
     const uint32_t* rank_codes;  // [slots][rank_stride]
     const uint32_t* rank_sorted; // [slots][rank_stride]
     int64_t rank_stride;
+    WalkOut walk;                // u16-coded wide launch after the walk pass (walk.meta null: none)
 };
 // wide complexes (65..kWideMaxPoints points, betti_wide.hip): per-wave scratch layout. Up to
 // kWideRegular points in the regular launch; above it (rank-coded: 10-bit vertices up to
@@ -174,14 +196,24 @@ struct WideLayout {
     int64_t guard;  // column-addition limit per column (a runaway-loop backstop)
     int64_t D, mc_e, mc_t, edges, adj, na_key, na_tau, na_tv, na_col, cl_list, vstore, vlist, h_key, h_meta,
         h_used, p1, p2, d0;
+    int64_t clb;     // prewalked layout: cleared-triangle bitmap [C(nmax, 3) bits] (mc_t and D empty)
+    int32_t prewalked;
 };
 // cap_limit > 0 (tests, DGN_DEBUG_WIDE_CAP): the regular layout's column / pivot / pair tables
 // hold at most cap_limit entries, so ordinary complexes overflow in the kernel and take the
 // capacity-retry path
 // grow (big only, 0..kWideMaxGrow): the capacity-retry level, tables of 2^(base_log2 + 2 grow) entries
-WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0, int grow = 0, int base_log2 = 24);
+WideLayout betti_wide_layout(int nmax, bool big = false, int64_t cap_limit = 0, int grow = 0, int base_log2 = 24,
+                             bool prewalked = false);
+// walk pass (betti_walk_kernel): one workgroup per complex of the slice list (bl.wide_list, its
+// device length bl.wide_len, u16 rank codes bl.rank_codes), outputs in bl.walk; `count` = the
+// slice's length bound (grid)
+constexpr int kWalkCap = 1 << 16;  // columns / cleared triangles per complex the walk pass lists (more: retry)
+WalkOut betti_walk_out_layout(int nmax);  // strides and cap (pointers null)
+int64_t betti_walk_out_bytes(int nmax);   // per complex
+hipError_t launch_betti_walk(hipStream_t s, const BettiLaunch& b, int64_t count, int nmax);
 hipError_t launch_betti_wide(hipStream_t s, const BettiLaunch& b, const WideLayout& l, int waves);
-int betti_wide_resident_waves(int device, int nmax, bool c16 = false);  // device-wide resident waves (occupancy API)
+int betti_wide_resident_waves(int device, int nmax, bool c16 = false, bool pre = false);  // device-wide resident waves (occupancy API)
 // rank codes for the complexes list[0..count) (retry slots): codes[r][t] = index of the first
 // occurrence of lower[list[r]][t] in the complex's sorted packed triangle (order- and
 // equality-preserving), sorted[r][...] = that sorted triangle (f32 bits). temp: caller-owned,

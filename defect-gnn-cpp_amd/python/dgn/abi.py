@@ -27,6 +27,7 @@ EXPORTS = [
     "dgn_debug_host_syncs", "dgn_debug_check_wide_layouts",
 ]
 DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP, DEBUG_BIG_LOG2, DEBUG_EMIT_CHUNK = 1, 2, 3, 4, 6, 7
+DEBUG_WIDE_WALK, DEBUG_SPLIT_CHUNK = 8, 9
 
 
 class DgnError(RuntimeError):
@@ -218,7 +219,7 @@ class Context:
 
     def set_debug(self, knob: int, value: int):
         """Debug / A-B knob (DEBUG_FORCE_RETRY, DEBUG_WIDE_WAVES, DEBUG_WIDE_C16, DEBUG_WIDE_CAP,
-        DEBUG_BIG_LOG2); tests and tools only."""
+        DEBUG_BIG_LOG2, DEBUG_EMIT_CHUNK, DEBUG_WIDE_WALK, DEBUG_SPLIT_CHUNK); tests and tools only."""
         self._check(lib().dgn_ctx_set_debug(self.h, knob, value), "set_debug")
 
     def retry_count(self) -> int:

@@ -68,7 +68,11 @@ int dgn_ctx_synchronize(dgn_ctx* ctx);
  *                        and are reduced again at the next levels (4x the tables each); 0 = natural;
  * DGN_DEBUG_EMIT_CHUNK   > 0: the large-row graph emit (per-wave key rows in HBM) launches this many
  *                        tiles at a time instead of its byte budget's count (its chunk loop on small
- *                        inputs); 0 = natural. */
+ *                        inputs); 0 = natural;
+ * DGN_DEBUG_WIDE_WALK    0 = the u16-coded wide complexes' whole apparent phase inside the per-wave
+ *                        wide kernel (default 1: the workgroup-per-complex walk pass before it);
+ * DGN_DEBUG_SPLIT_CHUNK  > 0: the component split of dgn_host_persistence[_lower] above 2,048 points
+ *                        takes at most this many clouds per chunk (its chunk loop on small inputs). */
 enum {
     DGN_DEBUG_FORCE_RETRY = 1,
     DGN_DEBUG_WIDE_WAVES = 2,
@@ -76,7 +80,9 @@ enum {
     DGN_DEBUG_WIDE_CAP = 4,
     /* 5: removed (the round-3 workgroup-per-complex kernel) */
     DGN_DEBUG_BIG_LOG2 = 6,
-    DGN_DEBUG_EMIT_CHUNK = 7
+    DGN_DEBUG_EMIT_CHUNK = 7,
+    DGN_DEBUG_WIDE_WALK = 8,
+    DGN_DEBUG_SPLIT_CHUNK = 9
 };
 int dgn_ctx_set_debug(dgn_ctx* ctx, int knob, int value);
 /* Diagnostics: complexes the capacity-retry launches reduced since the last call (synchronizes). */

@@ -260,3 +260,30 @@ def test_rank_code_tiers_dense_complexes(ctx):
         assert counts[c, 1] == r["n_inf0"], c
         for di, d in enumerate(("dim0", "dim1", "dim2")):
             assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+
+
+@pytest.mark.parametrize("thr", [np.inf, 1e39])
+def test_unbounded_threshold(ctx, thr):
+    """threshold = +inf (or a double above FLT_MAX, +inf after ripser_wrapper.cpp:28's cast):
+    every pair is an edge. The narrow rank codes must not take the lanes past the packed
+    triangle as edges (their mirrored stores would overwrite real codes). Clouds of
+    fewer points than their tier, through the main, dense and retry routes, vs the oracle."""
+    rng = np.random.default_rng(23)
+    sizes = [3, 17, 30, 31, 40, 44, 47, 60]
+    maxp = max(sizes)
+    clouds = np.zeros((len(sizes), maxp, 3))
+    npts = np.array(sizes, np.int32)
+    for c, n in enumerate(npts):
+        clouds[c, :n] = rng.uniform(0, 4, size=(n, 3))
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=4096)
+    for c, n in enumerate(npts):
+        r = O.persistence(O.local_distances(clouds[c, :n]), n, np.float32(np.inf))
+        assert counts[c, 1] == r["n_inf0"] == 1, c
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+    lows = np.zeros((len(sizes), maxp * (maxp - 1) // 2), np.float32)
+    for c, n in enumerate(npts):
+        low = O.local_distances(clouds[c, :n])
+        lows[c, :low.shape[0]] = low
+    pairs2, counts2 = ctx.host_persistence_lower(lows, npts, maxp, thr, cap=4096)
+    assert np.array_equal(counts2, counts) and np.array_equal(pairs2, pairs)

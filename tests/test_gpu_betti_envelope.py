@@ -321,6 +321,48 @@ def test_above_2048_points_split_into_components(ctx):
             assert np.array_equal(pl[c, di, :cl[c, col]], pairs[c, di, :counts[c, col]])
 
 
+def _many_small(rng, big, npair, nsingle, spread):
+    """One Gaussian cluster of `big` points, `npair` 2-point components and `nsingle` isolated points
+    on a 4 A grid beside it."""
+    clus = rng.uniform(0, 10, 3) + rng.normal(0, spread, (big, 3))
+    g = np.stack(np.meshgrid(np.arange(20), np.arange(20), np.arange(20)), -1).reshape(-1, 3) * 4.0 + np.array([40.0, 0, 0])
+    sel = rng.permutation(len(g))[:npair + nsingle]
+    a = g[sel[:npair]] + rng.normal(0, 0.05, (npair, 3))
+    b = a + rng.normal(0, 0.3, (npair, 3))
+    return np.vstack([clus, a, b, g[sel[npair:]]])
+
+
+def test_split_many_small_components_beside_a_large_one(ctx):
+    """The component split groups components by size (each group's triangle stride and pair block
+    are its largest member's, within a byte budget): clouds of ~5,000 points with one
+    ~1,100-point cluster, 1,500 two-point components and 1,000 isolated points, taken one cloud per
+    chunk (DGN_DEBUG_SPLIT_CHUNK = 1: the chunk loop), both input modes, against verbatim Ripser."""
+    rng = np.random.default_rng(41)
+    clouds = [_many_small(rng, 1100, 1500, 1000, 1.3), _many_small(rng, 900, 1600, 700, 1.6)]
+    npts = np.array([len(x) for x in clouds], np.int32)
+    m = int(npts.max())
+    C = np.zeros((len(clouds), m, 3))
+    for c, x in enumerate(clouds):
+        C[c, :len(x)] = x
+    thr = 1.0
+    ctx.set_debug(dgn.abi.DEBUG_SPLIT_CHUNK, 1)
+    try:
+        pairs, counts = ctx.host_persistence(C, npts, thr, cap=8192)
+        lows = [O.local_distances(x) for x in clouds]
+        L = np.zeros((len(clouds), m * (m - 1) // 2), np.float32)
+        for c, low in enumerate(lows):
+            L[c, :low.shape[0]] = low
+        pl, cl = ctx.host_persistence_lower(L, npts, m, thr, cap=8192)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_SPLIT_CHUNK, 0)
+    for c, n in enumerate(npts):
+        r = O.ref_persistence(lows[c], int(n), np.float32(thr))
+        assert counts[c, 1] == r["n_inf0"], c
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+    assert np.array_equal(cl, counts) and np.array_equal(pl, pairs)
+
+
 def test_above_2048_points_fails_loudly(ctx):
     # outside the envelope (DESIGN.md §8): an explicit DGN_ERR_UNSUPPORTED, never a silent or
     # truncated result -- a caller-given 2,100-point cloud whose threshold graph is one connected

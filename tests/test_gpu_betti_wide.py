@@ -150,3 +150,34 @@ def test_10A_fused_step_never_waits_for_the_host(ctx):
     bad = np.nonzero((cnt.cpu().numpy() != fx["fcc256_0/counts"]).any(axis=1))[0]
     assert bad.size == 0, bad[:8]
     np.testing.assert_allclose(feat.cpu().numpy(), fx["fcc256_0/features"], rtol=FEAT_RTOL, atol=FEAT_ATOL)
+
+
+def test_walk_pass_matches_per_wave_walk(ctx):
+    """The u16-coded wide complexes' dim-2 apparent walk as a workgroup-per-complex pass with the
+    code triangle in LDS (default) against the per-wave kernel's own walk (DGN_DEBUG_WIDE_WALK = 0):
+    identical counts, pairs and statistics; random clouds (with exact ties) of 65..362 points, both
+    against verbatim Ripser, and every atom of FCC-256 structure 0 at 10 A byte for byte."""
+    rng = np.random.default_rng(37)
+    sizes = [362, 65, 129, 200, 257, 330]
+    clouds = np.zeros((len(sizes), max(sizes), 3))
+    for c, n in enumerate(sizes):
+        clouds[c, :n] = rng.integers(0, 7, size=(n, 3)) if c % 2 else rng.uniform(0, 6.5, size=(n, 3))
+    npts = np.array(sizes, dtype=np.int32)
+    _check_clouds(ctx, clouds, npts, 1.9, 8192)
+    p1, k1 = ctx.host_persistence(clouds, npts, 1.9, cap=8192)
+    batch = dgn.synth_batch("fcc", 4, 1)
+    f1, c1 = ctx.host_betti(batch, 10.0)
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WALK, 0)
+    try:
+        p0, k0 = ctx.host_persistence(clouds, npts, 1.9, cap=8192)
+        f0, c0 = ctx.host_betti(batch, 10.0)
+    finally:
+        ctx.set_debug(dgn.abi.DEBUG_WIDE_WALK, 1)
+    assert np.array_equal(k0, k1)
+    for c in range(len(sizes)):
+        for d, col in ((0, 0), (1, 2), (2, 3)):
+            n = k1[c, col]
+            a0 = np.array(sorted(map(tuple, p0[c, d, :n])))
+            a1 = np.array(sorted(map(tuple, p1[c, d, :n])))
+            assert np.array_equal(a0, a1), (c, d)
+    assert np.array_equal(c0, c1) and np.array_equal(f0.view(np.uint64), f1.view(np.uint64))

@@ -1,0 +1,7 @@
+import sys
+p = sys.argv[1] + '/betti_wide.hip'
+s = open(p).read()
+o = "        reduce(1, nna1, 0);\n        if (err == 0u) reduce(2, nna2, base2);"
+assert s.count(o) == 1
+s = s.replace(o, "        (void)base2;")
+open(p, 'w').write(s)

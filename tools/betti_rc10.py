@@ -16,6 +16,8 @@ if os.environ.get("DGN_WIDE_WAVES"):
     ctx.set_debug(dgn.abi.DEBUG_WIDE_WAVES, int(os.environ["DGN_WIDE_WAVES"]))
 if os.environ.get("DGN_WIDE_C16"):
     ctx.set_debug(dgn.abi.DEBUG_WIDE_C16, int(os.environ["DGN_WIDE_C16"]))
+if os.environ.get("DGN_WIDE_WALK"):
+    ctx.set_debug(dgn.abi.DEBUG_WIDE_WALK, int(os.environ["DGN_WIDE_WALK"]))
 batch = dgn.synth_batch("fcc", 4, B)
 for r in range(reps):
     ctx.reset_timing()
