@@ -1377,6 +1377,8 @@ void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
 // are dropped when the reduction kernel reads the list). No dim-2 min-cofacet table: the reduction
 // decides apparent owners from the matrix (lookup, PRE form).
 constexpr int kWalkWaves = 16;
+constexpr int kWalkRing = 128;  // queued triangles per wave (refilled below 64: at most 63 + 64 held)
+__device__ __forceinline__ uint32_t c2u(int x) { return ((uint32_t)x * (uint32_t)(x - 1)) >> 1; }
 __device__ __forceinline__ uint32_t walk_ticket(uint32_t* ctr) {  // wave-uniform, no branch on the lane
     const uint32_t t = atomicAdd(ctr, lane_id() == 0 ? 1u : 0u);
     return (uint32_t)__builtin_amdgcn_readlane((int)t, 0);
@@ -1405,11 +1407,14 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
     const int W = (n + 63) / 64;
     const int wmax = (wo.nmax + 63) / 64;
     const int np4 = (wo.nmax + 3) & ~3;
-    uint64_t* adj = walk_lds;                                              // [n][W]
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(walk_lds + wo.nmax * wmax);  // kWc* counters
-    uint16_t* par = reinterpret_cast<uint16_t*>(ctr + 8);                  // forest parents, 0xFFFF = root
-    uint16_t* d0c = par + np4;                                             // dim-0 death codes
-    uint16_t* T = d0c + np4;                                               // packed codes, row i at c2(i)
+    // LDS: the packed codes at offset 0 (row i at c2(i)), then the bitsets, counters, forest
+    // parents, dim-0 death codes and the per-wave triangle rings
+    uint16_t* T = reinterpret_cast<uint16_t*>(walk_lds);
+    uint64_t* adj = walk_lds + ((int64_t)wo.nmax * (wo.nmax - 1) / 2 + 3) / 4;  // [n][W]
+    uint32_t* ctr = reinterpret_cast<uint32_t*>(adj + wo.nmax * wmax);          // kWc* counters
+    uint16_t* par = reinterpret_cast<uint16_t*>(ctr + 8);                      // forest parents, 0xFFFF = root
+    uint16_t* d0c = par + np4;                                                 // dim-0 death codes
+    uint32_t* rings = reinterpret_cast<uint32_t*>(d0c + np4);                  // [kWalkWaves][kWalkRing]
     const uint32_t* vals = bl.rank_sorted + wi * bl.rank_stride;           // code -> f32 bits
     for (int i = threadIdx.x; i < n * W; i += kWave * kWalkWaves) adj[i] = 0ull;
     if (threadIdx.x < 8) ctr[threadIdx.x] = 0u;
@@ -1599,24 +1604,26 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
         }
     }
     // (4) the dim-2 walk. Each wave takes top vertices a (descending: the largest share of triangles
-    // first) from an LDS cursor and deals the triangles (a, b, c), c < b < a, of a's edges to its
-    // lanes as the per-wave kernel's pass_dim2 does from its edge list; a lane whose walk ended
-    // takes the next triangle at once.
+    // first) from an LDS cursor and queues the triangles (a, b, c), c < b < a, of a's edges in a
+    // per-wave LDS ring (one common-neighbour word of an edge per refill step: the lanes holding its
+    // set bits store them at their prefix count); a lane whose walk ended takes the next queued
+    // triangle at once (pass_dim2's dealing, without its per-lane bit selects).
     uint64_t* oent = wo.ent + wi * (int64_t)wo.cap;
+    uint32_t* ring = rings + wv * kWalkRing;
     int ca = -1, cb = 0, cw = 0, bw = 0;  // cursor (uniform): edge (ca, cb), word cw of its c's
-    uint64_t cm = 0, bm = 0;              // c's of word cw not yet dealt; b's of row ca word bw not yet taken
+    uint64_t bm = 0;                      // b's of row ca word bw not yet taken
     bool exhausted = false;
+    int head = 0, tail = 0;               // the ring's uniform read / write counts
     int ea = 0, eb = 0, c = 0, w = 0, bk = -1;
-    int ra = 0, rb = 0, rcc = 0;  // c2 of the lane's triangle's vertices
+    uint32_t ra = 0, rb = 0, rcc = 0;     // c2 of the lane's triangle's vertices
     bool act = false, fresh = false, found = false;
     uint64_t m = 0;
     uint32_t bd = 0xFFFFFFFFu, ds = 0, dab = 0, dac = 0, dbc = 0, hda = 0, hdb = 0, hdc = 0;
     for (;;) {
-        for (;;) {  // lanes without a triangle take the next ones, in order
-            const uint64_t need = ballot(!act);
-            if (!need) break;
-            while (cm == 0ull && !exhausted) {
-                if (ca >= 0 && cb > 0 && 64 * (cw + 1) < cb) {
+        while (tail - head < kWave && !exhausted) {  // refill: the next edge word with a common neighbour
+            uint64_t mm = 0;
+            for (;;) {
+                if (cb > 0 && 64 * (cw + 1) < cb) {
                     ++cw;
                 } else {
                     while (bm == 0ull) {  // the next b of row ca, or the next top vertex
@@ -1640,30 +1647,39 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
                     bm &= bm - 1ull;
                     cw = 0;
                 }
-                uint64_t mm = uniw64(aw(ca, cw) & aw(cb, cw));
+                mm = uniw64(aw(ca, cw) & aw(cb, cw));
                 const int lim = cb - 64 * cw;
                 if (lim < 64) mm &= (1ull << lim) - 1ull;
-                cm = mm;
+                if (mm) break;
             }
-            if (cm == 0ull) break;  // every triangle dealt
-            const int p = __popcll(cm), q = __popcll(need);
+            if (exhausted) break;
+            if ((mm >> lane) & 1ull)
+                ring[(tail + mask_prefix(mm)) & (kWalkRing - 1)] =
+                    ((uint32_t)ca << 18) | ((uint32_t)cb << 9) | (uint32_t)(64 * cw + lane);
+            tail += __popcll(mm);
+        }
+        wave_lds_order();
+        {  // idle lanes take queued triangles, in order
+            const uint64_t need = ballot(!act);
+            const int avail = tail - head;
             const int r = mask_prefix(need);
-            if (!act && r < p) {
-                c = 64 * cw + H::select_bit(cm, r);
-                ea = ca;
-                eb = cb;
+            if (!act && r < avail) {
+                const uint32_t t = ring[(head + r) & (kWalkRing - 1)];
+                ea = (int)(t >> 18);
+                eb = (int)((t >> 9) & 511u);
+                c = (int)(t & 511u);
                 act = fresh = true;
             }
-            cm = q >= p ? 0ull : cm & ~((1ull << H::select_bit(cm, q)) - 1ull);
+            head += min(__popcll(need), avail);
         }
-        if (!ballot(act)) break;
+        if (!ballot(act)) break;  // nothing queued, nothing left to queue
         bool na = false;
         uint64_t ent = 0;
         if (act) {
             if (fresh) {
-                ra = c2i(ea);
-                rb = c2i(eb);
-                rcc = c2i(c);
+                ra = c2u(ea);
+                rb = c2u(eb);
+                rcc = c2u(c);
                 dab = T[ra + eb];
                 dac = T[ra + c];
                 dbc = T[rb + c];
@@ -1675,48 +1691,45 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
                 found = false;
                 fresh = false;
             }
-            constexpr int kS = 4;  // candidates per step, highest first
+            while (m == 0ull && w > 0) {  // the next word with a common neighbour of a, b, c
+                --w;
+                m = aw(ea, w) & aw(eb, w) & aw(c, w);
+            }
+            // up to kS candidates of this word, highest first
+            constexpr int kS = 4;
             int kk[kS];
             bool val[kS];
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
-                while (m == 0ull && w > 0) {
-                    --w;
-                    m = aw(ea, w) & aw(eb, w) & aw(c, w);
-                }
                 val[j] = m != 0ull;
-                const int bit = val[j] ? 63 - __clzll((long long)m) : 0;
-                kk[j] = 64 * w + bit;
-                if (val[j]) m &= ~(1ull << bit);
+                const int bit = 63 - __clzll((long long)(m | 1ull));
+                kk[j] = val[j] ? 64 * w + bit : c;  // d(c, c) reads a harmless in-range entry
+                m &= ~(1ull << bit);
             }
             uint32_t da[kS], dbv[kS], dc[kS];
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
-                const int k = val[j] ? kk[j] : c;  // d(c, c): a harmless in-range read
-                const int ck = c2i(k);
-                da[j] = dd(ea, ra, k, ck);
-                dbv[j] = dd(eb, rb, k, ck);
-                dc[j] = dd(c, rcc, k, ck);
+                const int k = kk[j];
+                const uint32_t ck = c2u(k);
+                da[j] = T[k < ea ? ra + k : ck + ea];
+                dbv[j] = T[k < eb ? rb + k : ck + eb];
+                dc[j] = T[k < c ? rcc + k : ck + c];
             }
             // (diameter, k) only: walking k downwards a smaller k wins only with a strictly smaller
             // diameter (pass_dim2)
 #pragma unroll
             for (int j = 0; j < kS; ++j) {
-                if (!val[j] || found) continue;
                 const uint32_t dk = max(max(da[j], dbv[j]), dc[j]);
-                if (dk <= ds) {
-                    bd = ds;
-                    bk = kk[j];
-                    found = true;
-                    hda = da[j];
-                    hdb = dbv[j];
-                    hdc = dc[j];
-                } else if (dk < bd) {
-                    bd = dk;
-                    bk = kk[j];
-                }
+                const bool z = val[j] && !found && dk <= ds;
+                const bool lt = val[j] && !found && dk < bd;
+                hda = z ? da[j] : hda;
+                hdb = z ? dbv[j] : hdb;
+                hdc = z ? dc[j] : hdc;
+                bk = z || lt ? kk[j] : bk;
+                bd = z ? ds : (lt ? dk : bd);
+                found = found || z;
             }
-            if (found || !val[kS - 1]) {
+            if (found || (m == 0ull && w == 0)) {
                 act = false;
                 if (bk >= 0) {
                     const uint32_t colp = ((uint32_t)ea << 18) | ((uint32_t)eb << 9) | (uint32_t)c;
@@ -1745,7 +1758,8 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
 
 size_t walk_lds_bytes(int nmax) {
     const int64_t wmax = (nmax + 63) / 64, np4 = (nmax + 3) & ~3;
-    return (size_t)(8 * nmax * wmax + 32 + 2 * 2 * np4 + 2 * ((int64_t)nmax * (nmax - 1) / 2) + 8);
+    return (size_t)(8 * (((int64_t)nmax * (nmax - 1) / 2 + 3) / 4) + 8 * nmax * wmax + 32 + 2 * 2 * np4 +
+                    4 * kWalkWaves * kWalkRing);
 }
 
 int64_t align256(int64_t x) { return (x + 255) / 256 * 256; }

@@ -149,6 +149,8 @@ struct dgn_ctx {
     int dbg_wide_waves = 0;        // cap on the wide launch's resident waves (0 = none)
     int dbg_wide_cap = 0;          // regular wide layout's column / pivot / pair table cap (0 = natural)
     bool dbg_wide_c16 = true;      // u16 rank codes for wide complexes of <= kC16MaxPoints points
+    hipStream_t rstream = nullptr;  // the 10 A reductions beside the next slice's walk pass
+    hipEvent_t ev_walk[2] = {nullptr, nullptr}, ev_red[2] = {nullptr, nullptr};
     bool dbg_wide_walk = true;     // the u16-coded complexes' dim-2 walk as a workgroup-per-complex pass
     int dbg_split_chunk = 0;       // clouds per chunk of the component split (0 = its byte budget)
     int dbg_big_log2 = 0;          // capacity-retry layout's first-level table size log2 (0 = natural 24)
@@ -587,34 +589,54 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                     const int64_t rstride = ((int64_t)max_points * (max_points - 1) / 2 + 63) / 64 * 64;
                     int64_t slice = std::max<int64_t>(
                         1, std::min<int64_t>({nwide, (int64_t(16) << 30) / (20 * rstride), INT32_MAX / rstride}));
-                    // the walk pass's per-complex outputs (matrix, bitsets, dim-2 column list: ~2 MB at
-                    // 340 points) within a quarter of the HBM that is free or already theirs, <= 32 GB
+                    // The walk pass's per-complex outputs (matrix, lists: ~1.7 MB at 340 points), two
+                    // slices' worth within a quarter of the HBM that is free or already theirs, <= 32 GB.
+                    // Slice q's walk pass (LDS- and issue-bound, one workgroup per CU) runs on the context
+                    // stream while slice q - 1's reductions (LDS-free, latency-bound) run on a second
+                    // stream: double-buffered codes and walk outputs, ordered by events
                     const int64_t walk_bytes = prewalk ? betti_walk_out_bytes(max_points) : 0;
+                    const int nbuf = prewalk ? 2 : 1;
                     if (prewalk) {
                         size_t free_b = 0, total_b = 0;
                         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
                         const int64_t wbudget = std::min<int64_t>(
                             int64_t(32) << 30, std::max<int64_t>(int64_t(1) << 30, ((int64_t)free_b + (int64_t)c->b_walk.bytes) / 4));
-                        slice = std::max<int64_t>(1, std::min<int64_t>(slice, wbudget / walk_bytes));
+                        slice = std::max<int64_t>(1, std::min<int64_t>(slice, wbudget / (nbuf * walk_bytes)));
                     }
                     // equal slices: a short last slice leaves its launch's resident waves idle behind
                     // a tail of single complexes
                     slice = (nwide + (nwide + slice - 1) / slice - 1) / ((nwide + slice - 1) / slice);
-                    if (prewalk) HIP_TRY(c, c->b_walk.ensure((size_t)walk_bytes * (size_t)slice));
                     const size_t tmp_bytes = betti_rank_temp_bytes(slice, rstride);
-                    HIP_TRY(c, c->b_rank16.ensure(8 * (size_t)slice * rstride + tmp_bytes));
+                    const size_t rank_buf = (8 * (size_t)slice * rstride + tmp_bytes + 255) / 256 * 256;
+                    const size_t walk_buf = ((size_t)walk_bytes * (size_t)slice + 255) / 256 * 256;
+                    if (prewalk) HIP_TRY(c, c->b_walk.ensure(walk_buf * nbuf));
+                    HIP_TRY(c, c->b_rank16.ensure(rank_buf * nbuf));
                     const int64_t nsl = (nwide + slice - 1) / slice;
                     HIP_TRY(c, c->b_rscal16.ensure(sizeof(uint32_t) * 2 * (size_t)nsl));
                     uint32_t* sl = c->b_rscal16.as<uint32_t>();
                     HIP_TRY(c, launch_slice_lengths(c->stream, &sc->wide_len, slice, nsl, sl));
-                    uint32_t* codes = c->b_rank16.as<uint32_t>();
-                    uint32_t* sorted = codes + slice * rstride;
+                    hipStream_t rs = c->stream;  // the reductions' stream
+                    if (prewalk && nsl > 1) {
+                        if (!c->rstream) {
+                            HIP_TRY(c, hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+                            for (int k = 0; k < 2; ++k) {
+                                HIP_TRY(c, hipEventCreateWithFlags(&c->ev_walk[k], hipEventDisableTiming));
+                                HIP_TRY(c, hipEventCreateWithFlags(&c->ev_red[k], hipEventDisableTiming));
+                            }
+                        }
+                        rs = c->rstream;
+                    }
                     for (int64_t q = 0; q < nsl; ++q) {
+                        const int k = (int)(q % nbuf);
+                        uint32_t* codes = reinterpret_cast<uint32_t*>(c->b_rank16.as<uint8_t>() + k * rank_buf);
+                        uint32_t* sorted = codes + slice * rstride;
                         BettiLaunch wb = pb;
                         wb.wide_list = c->b_wlist.as<int32_t>() + q * slice;
                         wb.wide_len = sl + 2 * q;
                         wb.wide_queue = sl + 2 * q + 1;
                         const int64_t ub = std::min<int64_t>(slice, nwide - q * slice);
+                        // buffer k was last read by slice q - 2's reductions
+                        if (rs != c->stream && q >= 2) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_red[k], 0));
                         HIP_TRY(c, betti_rank_codes(c->stream, pb.lower, pb.tri_stride, pb.npoints, wb.wide_list, ub,
                                                     rstride, codes, sorted, sorted + slice * rstride, tmp_bytes,
                                                     wb.wide_len));
@@ -623,11 +645,11 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                         wb.rank_stride = rstride;
                         if (prewalk) {
                             WalkOut wo = betti_walk_out_layout(max_points);
-                            uint8_t* p = c->b_walk.as<uint8_t>();
+                            uint8_t* p = c->b_walk.as<uint8_t>() + k * walk_buf;
                             auto carve = [&](int64_t bytes_per_complex) {
-                                uint8_t* q = p;
+                                uint8_t* r = p;
                                 p += (size_t)bytes_per_complex * (size_t)slice;
-                                return q;
+                                return r;
                             };
                             wo.dmat = reinterpret_cast<uint16_t*>(carve(2 * wo.dstride));
                             wo.meta = reinterpret_cast<uint32_t*>(carve(32));
@@ -639,7 +661,16 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                             wb.walk = wo;
                             HIP_TRY(c, launch_betti_walk(c->stream, wb, ub, max_points));
                         }
-                        HIP_TRY(c, launch_betti_wide(c->stream, wb, wl, (int)std::min<int64_t>(wide_waves, ub)));
+                        if (rs != c->stream) {
+                            HIP_TRY(c, hipEventRecord(c->ev_walk[k], c->stream));
+                            HIP_TRY(c, hipStreamWaitEvent(rs, c->ev_walk[k], 0));
+                        }
+                        HIP_TRY(c, launch_betti_wide(rs, wb, wl, (int)std::min<int64_t>(wide_waves, ub)));
+                        if (rs != c->stream) HIP_TRY(c, hipEventRecord(c->ev_red[k], rs));
+                    }
+                    if (rs != c->stream) {  // join: the retry launch and the outputs follow on the context stream
+                        HIP_TRY(c, hipEventRecord(c->ev_red[0], rs));
+                        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_red[0], 0));
                     }
                 }
             }
@@ -932,6 +963,12 @@ void dgn_ctx_destroy(dgn_ctx* c) {
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->rstream) (void)hipStreamSynchronize(c->rstream);
+    for (int k = 0; k < 2; ++k) {
+        if (c->ev_walk[k]) (void)hipEventDestroy(c->ev_walk[k]);
+        if (c->ev_red[k]) (void)hipEventDestroy(c->ev_red[k]);
+    }
+    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     if (c->host) (void)hipHostFree(c->host);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;  // DevBuf destructors free the device workspaces
