@@ -15,10 +15,11 @@
 //     (ripser.cpp:318-324, 386-395), the f32 values come back from the sorted table only for
 //     the emitted pairs. 2 B per entry keep a 48-point complex in 5 KB of LDS (eight waves per
 //     SIMD instead of five with the f32 matrix);
-//   * distance matrix: the K=3 Gram product is built on the matrix cores with
-//     v_mfma_f64_16x16x4_f64 as three rank-1 products (exactly round(x_ik*x_jk) each), summed on
-//     the VALU in the reference's order ((p0+p1)+p2), then sqrt(max(0,(sq_i+sq_j)-2p)) -> f32:
-//     bit-identical to the reference's Eigen/SSE2 arithmetic;
+//   * distance matrix (the distance kernels, dgn_device.hpp gram_triangle_*): the K = 3 Gram product
+//     with every product rounded, summed in the reference's order ((p0+p1)+p2), then
+//     sqrt(max(0,(sq_i+sq_j)-2p)) -> f32, bit-identical to the reference's Eigen/SSE2 arithmetic --
+//     one packed pair per lane on the f64 VALU for n <= 64 (round 5: measured faster than 16x16
+//     v_mfma_f64 tiles, 5.94 -> 4.20 ms per config-4 shard), matrix-core tiles above 64 points;
 //   * dim 0: Prim on F-keys (diameter, then combinatorial index descending) == Kruskal's unique
 //     minimum spanning forest in Ripser's order (ripser.cpp:725-762);
 //   * dim 1 and dim 2: cohomology with clearing. One lane per column finds its pivot (F-minimal
@@ -1313,12 +1314,12 @@ __global__ __launch_bounds__(256) void betti_dist_kernel(BettiLaunch bl, DistLau
                 x[0] = cloud[3 * p];
                 x[1] = cloud[3 * p + 1];
                 x[2] = cloud[3 * p + 2];
-            });
+            }, bl.tri_stride);
             continue;
         }
         const int pl = lane < n ? lane : n - 1;
         const double px[3] = {cloud[3 * pl], cloud[3 * pl + 1], cloud[3 * pl + 2]};
-        gram_triangle_narrow(px, n, sq, L);
+        gram_triangle_narrow(px, n, sq, L, bl.tri_stride);
     }
 }
 

@@ -12,8 +12,8 @@
 // component; a single component above that stays outside the envelope (DGN_ERR_UNSUPPORTED).
 //
 //   big_gram_kernel        distances of clouds above 2,048 points (the reference's Gram arithmetic,
-//                          ripser_wrapper.cpp:64-67, on the VALU: the same rounded products the MFMA
-//                          tiles of the ordinary path produce), f32 packed lower triangle
+//                          ripser_wrapper.cpp:64-67, on the VALU: the same rounded products and sums
+//                          as the ordinary distance kernels), f32 packed lower triangle
 //   components_kernel      union-find over the pairs d <= thr (one workgroup per complex; roots
 //                          link larger -> smaller with a compare-and-swap, so parents only decrease)
 //   gather_sub_kernel      a component's packed sub-triangle (vertices in ascending order)

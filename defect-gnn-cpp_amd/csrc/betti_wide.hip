@@ -721,28 +721,29 @@ struct WideCx {
         }
         return kNoMetaW;
     }
-    __device__ bool hinsert(uint64_t k, uint64_t meta, int npiv) {
+    // insert k at `fslot`, the first empty slot of k's probe window as the column's last lookup
+    // saw it (nothing was inserted since), or probe for one (fslot = ~0: that window was full). No
+    // fence here: the caller's one fence covers this and the column's other stores
+    __device__ bool hinsert(uint64_t k, uint64_t meta, int npiv, uint32_t fslot) {
         const int lane = lane_id();
         uint64_t* HK = sp<uint64_t>(ly.h_key);
         uint64_t* HM = sp<uint64_t>(ly.h_meta);
         const uint32_t mask = (uint32_t)ly.h_cap - 1u;
         const uint32_t base = hmix(k) & mask;
         if (npiv >= ly.na_cap) return false;
-        for (int probe = 0; probe < ly.h_cap; probe += kWave) {
+        uint32_t slot = fslot;
+        for (int probe = 0; slot == ~0u && probe < ly.h_cap; probe += kWave) {
             const uint64_t x = HK[(base + (uint32_t)(probe + lane)) & mask];
             const uint64_t emp = ballot(x == 0ull);
-            if (emp) {
-                const uint32_t slot = (base + (uint32_t)(probe + __ffsll((unsigned long long)emp) - 1)) & mask;
-                if (lane == 0) {
-                    HK[slot] = k;
-                    HM[slot] = meta;
-                    sp<uint32_t>(ly.h_used)[npiv] = slot;
-                }
-                wave_scratch_sync();  // the next lookups (other lanes) see it
-                return true;
-            }
+            if (emp) slot = (base + (uint32_t)(probe + __ffsll((unsigned long long)emp) - 1)) & mask;
         }
-        return false;
+        if (slot == ~0u) return false;
+        if (lane == 0) {
+            HK[slot] = k;
+            HM[slot] = meta;
+            sp<uint32_t>(ly.h_used)[npiv] = slot;
+        }
+        return true;
     }
 
     // Owner of the pivot tau in one round trip where possible: the first 64-slot window of the
@@ -751,7 +752,7 @@ struct WideCx {
     // F-max facet f if tau is f's F-minimal cofacet (recorded by the lane-parallel pass; tree edges
     // and cleared triangles hold kMcNone), decided from the edge lengths already in registers and
     // one min-cofacet table read. Returns kNoMetaW when tau is not in the table.
-    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, PT& app) const {
+    __device__ uint64_t lookup(int dim, uint64_t tau, uint64_t tv, PT& app, uint32_t& fslot) const {
         const int lane = lane_id();
         const uint64_t* HK = sp<uint64_t>(ly.h_key);
         const uint64_t* HM = sp<uint64_t>(ly.h_meta);
@@ -773,10 +774,13 @@ struct WideCx {
         const int fh = hit ? __ffsll((unsigned long long)hit) - 1 : kWave;
         const int fe = emp ? __ffsll((unsigned long long)emp) - 1 : kWave;
         app = kNoneP;
+        fslot = ~0u;
         if (fh < fe) return rlw64(hm, fh);
         if (fe == kWave) {  // the window was full: probe on (rare at load factor <= 1/2)
             const uint64_t m = hfind(tau);
             if (m != kNoMetaW) return m;
+        } else {
+            fslot = (hmix(tau) + (uint32_t)fe) & mask;
         }
         uint32_t dd[4][4];
         if (nv == 4) {
@@ -823,7 +827,9 @@ struct WideCx {
                 // to f within diam f (the all-ones diagonal excludes f's vertices). Decided from
                 // f's three rows (coalesced), words from vd's on; such a pair is always apparent
                 // (diam tau = diam f and f its F-max facet), and a cleared f (a dim-1 pivot) is
-                // never in one, so no min-cofacet table or clearing state is needed.
+                // never in one, so no min-cofacet table or clearing state is needed. (Loading the
+                // four rows of tau together with the table window instead -- one round trip less
+                // -- measured slower: 24 loads and 51 spilled VGPRs per lookup)
                 const int fa = pv(bestf, 2), fb = pv(bestf, 1), fc = pv(bestf, 0);
                 const uint32_t fd = kdiam(bestk);
                 const int t0 = vd >> 6;
@@ -1016,14 +1022,30 @@ struct WideCx {
         int& np = dim == 1 ? n_p1 : n_p2;
         int npiv = 0;
         int64_t vused = 0;
+        // the next column's record is loaded while this one is reduced (its load is not on the chain)
+        uint64_t nK = 0, nT = 0, nV = 0;
+        PT nC = 0;
+        if (nna > 0) {
+            nK = K[0];
+            nT = T[0];
+            nV = V[0];
+            nC = Cc[0];
+        }
         for (int ci = 0; ci < nna && err == 0u; ++ci) {
-            const uint64_t colkey = uniw64(K[ci]);
-            uint64_t tau = uniw64(T[ci]);
-            uint64_t tv = uniw64(V[ci]);
-            const PT cp = unip(Cc[ci]);
+            const uint64_t colkey = uniw64(nK);
+            uint64_t tau = uniw64(nT);
+            uint64_t tv = uniw64(nV);
+            const PT cp = unip(nC);
+            if (ci + 1 < nna) {
+                nK = K[ci + 1];
+                nT = T[ci + 1];
+                nV = V[ci + 1];
+                nC = Cc[ci + 1];
+            }
             const uint32_t birth = kdiam(colkey);
             PT app;
-            uint64_t meta = lookup(dim, tau, tv, app);
+            uint32_t fslot;
+            uint64_t meta = lookup(dim, tau, tv, app, fslot);
             int v = 0;  // 0 = lazy: V == {this column}
             vspill = !VREG;
             if (meta != kNoMetaW || app != kNoneP) {
@@ -1050,7 +1072,7 @@ struct WideCx {
                     }
                     tau = v > 0 ? pivot_of_V(dim, v, tau, tv) : kInfW;
                     if (tau == kInfW) break;  // zero column: essential class, not emitted
-                    meta = lookup(dim, tau, tv, app);
+                    meta = lookup(dim, tau, tv, app, fslot);
                     if (meta == kNoMetaW && app == kNoneP) break;  // tau is this column's pivot
                     if (++guard > ly.guard) {
                         err |= kEGuard;
@@ -1087,15 +1109,17 @@ struct WideCx {
                 } else if (lane < v) {
                     vstore[vused + lane] = vreg;
                 }
-                wave_scratch_sync();
                 m = ((uint64_t)vused << kMetaLenBits) | (uint64_t)v;
                 vused += v;
             }
-            if (!hinsert(tau, m, npiv)) {
+            if (!hinsert(tau, m, npiv, fslot)) {
                 err |= kEPiv;
                 break;
             }
             ++npiv;
+            // one fence for the column's stores (V store, pivot table, pair, clearing mark): the next
+            // lookups and owner toggles (other lanes) read them
+            wave_scratch_sync();
         }
         wave_scratch_sync();
         // empty the pivot table for the next dimension / complex

@@ -836,7 +836,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         int st = vr_pass(0, A, lower, (int64_t)cloud_stride * (cloud_stride - 1) / 2, npoints, nullptr, 0.0);
         if (st) return st;
     } else {
-        // distance pass (MFMA) + Betti pass per chunk of complexes; the triangle buffer is
+        // distance pass (f64 VALU pairs; matrix cores above 64 points) + Betti pass per chunk of complexes; the triangle buffer is
         // bounded (~16 GB of the 288 GB HBM) so arbitrarily large shards stream through it
         const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(A, (int64_t(16) << 30) / (4 * tri_stride)));
         HIP_TRY(c, c->b_lower.ensure(sizeof(float) * (size_t)(chunk * tri_stride)));

@@ -111,6 +111,15 @@ __device__ __forceinline__ void dgn_check_full_exec() {
     if (__builtin_amdgcn_read_exec() != ~0ull) __builtin_trap();
 #endif
 }
+// Bounds checks of stores whose index a kernel derives (DGN_DEVICE_CHECKS builds only: a trap
+// names the faulting kernel in the HIP error instead of a write past the buffer)
+__device__ __forceinline__ void dgn_check(bool ok) {
+#if defined(DGN_DEVICE_CHECKS) && DGN_DEVICE_CHECKS
+    if (!ok) __builtin_trap();
+#else
+    (void)ok;
+#endif
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
     dgn_check_full_exec();
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)x, 0x121, 0xf, 0xf, false));
@@ -179,9 +188,12 @@ constexpr double kLeanSqrtMin = 0x1p-767;  // the compiler's rescaling threshold
 // computes a wanted distance and the stores are contiguous (a 16 x 16 Gram tile on the matrix
 // cores leaves 37 % of the lanes idle at n = 43 and its products need the same VALU tail: the
 // MFMA form measured 4.55 ms of the 5.94 ms config-4 distance kernel, the search 1.39 ms).
-__device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, double* rec, float* __restrict__ L) {
+// cap: floats the caller reserved for this complex's triangle (bounds check of DGN_DEVICE_CHECKS builds)
+__device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, double* rec, float* __restrict__ L,
+                                                     int64_t cap) {
     typedef double double2_t __attribute__((ext_vector_type(2)));
     const int lane = lane_id();
+    dgn_check(n >= 1 && n <= kWave && tri_c2(n) <= cap);
     const double sq = (px[0] * px[0] + px[1] * px[1]) + px[2] * px[2];  // rowwise().squaredNorm()
     wave_lds_sync();
     if (lane < n) {
@@ -206,7 +218,10 @@ __device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, 
         double dd;
         if (ballot(!(d2 >= kLeanSqrtMin && d2 < __builtin_inf()))) dd = sqrt(d2);
         else dd = sqrt_lean(d2);
-        if (base + lane < tot) L[t] = (float)dd;
+        if (base + lane < tot) {
+            dgn_check(t < (uint32_t)tot && j < i);
+            L[t] = (float)dd;
+        }
     }
     wave_lds_sync();
 }
@@ -215,9 +230,10 @@ __device__ __forceinline__ void gram_triangle_narrow(const double px[3], int n, 
 // indices only); sq = LDS [n].
 __device__ __forceinline__ double sel3(int k, double a, double b, double c) { return k == 0 ? a : (k == 1 ? b : c); }
 template <class Point>
-__device__ __forceinline__ void gram_triangle_wide(int n, double* sq, float* __restrict__ L, Point&& point) {
+__device__ __forceinline__ void gram_triangle_wide(int n, double* sq, float* __restrict__ L, Point&& point, int64_t cap) {
     typedef double double4_t __attribute__((ext_vector_type(4)));
     const int lane = lane_id();
+    dgn_check((int64_t)n * (n - 1) / 2 <= cap);
     const int kq = lane >> 4;
     for (int p = lane; p < n; p += kWave) {
         double x[3];
@@ -250,6 +266,7 @@ __device__ __forceinline__ void gram_triangle_wide(int n, double* sq, float* __r
             for (int r = 0; r < 4; ++r) {
                 const int row = 16 * I + (lane >> 4) + 4 * r;
                 if (row < n && cb < row) {
+                    dgn_check(tri_c2(row) + cb < tri_c2(n));
                     const double dot = (p0[r] + p1[r]) + p2[r];
                     const double d2 = (sq[row] + sq[cb]) - 2.0 * dot;
                     L[tri_c2(row) + cb] = (float)sqrt(fmax(d2, 0.0));

@@ -1887,7 +1887,7 @@ __global__ __launch_bounds__(kGraphBlock) void graph_emit_kernel(GraphLaunch g, 
 // order instead of the sorted one. Writes the f32 lower triangle (the reference's Gram arithmetic,
 // gram_triangle_*) + npoints.
 // ------------------------------------------------------------------------------------------
-// The Betti search + MFMA distance kernel writes ~1 KB of triangle per complex with little reuse:
+// The Betti search + distance kernel (f64 VALU pairs for n <= 64, matrix-core tiles above) writes ~1 KB of triangle per complex with little reuse:
 // compiled for 4 waves per SIMD (128 VGPRs, a few spills) it keeps more stores in flight than at
 // its natural 161 VGPRs (3 waves): 7.6 -> 5.9 ms per config-4 shard (tools/ab_dist.sh)
 // (the 64-point instantiation; the wide ones are LDS-bound anyway). A 256-thread block is one wave
@@ -1993,9 +1993,9 @@ __global__ __launch_bounds__(kGraphBlock, CAP <= kWave ? DGN_DIST_WPE : 1) void 
         if (n <= kWave) {
             double px[3];
             point(lane < n ? lane : n - 1, px);
-            gram_triangle_narrow(px, n, cloud_s[w], L);
+            gram_triangle_narrow(px, n, cloud_s[w], L, tri_stride);
         } else {
-            gram_triangle_wide(n, cloud_s[w] + CAP, L, point);
+            gram_triangle_wide(n, cloud_s[w] + CAP, L, point, tri_stride);
         }
     });
 }

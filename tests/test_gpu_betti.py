@@ -1,4 +1,4 @@
-"""HIP Betti path (MFMA distances + wave-parallel VR reduction + statistics) through the C ABI
+"""HIP Betti path (Gram distances + wave-parallel VR reduction + statistics) through the C ABI
 vs the oracle and the verbatim-Ripser golden fixtures. Counts and pairs bit-exact; the 35
 statistics within 1e-6 relative (absolute floor 1e-12: std of near-constant sets)."""
 import os
@@ -206,7 +206,7 @@ def _kernel_vs_reference_triangles(lower, npts, keys, lat, pos, a, rc):
 
 @pytest.mark.parametrize("s", [0, 3, 7])
 def test_betti_dist_triangles_sc64_fixture(ctx, s):
-    """The Betti pass's own neighbour search + MFMA Gram distances: every entry of the f32 lower
+    """The Betti pass's own neighbour search + Gram distances (f64 VALU pairs): every entry of the f32 lower
     triangle bit-identical to the reference arithmetic (sc64_rc5.npz lower0 / lower37, i.e.
     ripser_wrapper.cpp:20-24 over betti_features.cpp:67-73's cloud)."""
     fx = np.load(os.path.join(GOLDEN, "sc64_rc5.npz"))

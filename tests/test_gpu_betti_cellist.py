@@ -92,7 +92,7 @@ def test_triclinic_688_every_atom(ctx):
 
 
 def test_sc4096_search_triangles(ctx):
-    """The cell-list search + MFMA Gram triangles of SC-4096 atoms (corners, faces, interior)
+    """The cell-list search + Gram triangles (f64 VALU pairs) of SC-4096 atoms (corners, faces, interior)
     bit-identical to the reference arithmetic over the oracle's NeighborList(5, inf)."""
     batch = dgn.synth_batch("sc", 16, 1)
     lat, pos = batch["lattice"][0], batch["positions"]
