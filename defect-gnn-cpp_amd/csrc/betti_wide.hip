@@ -1378,8 +1378,11 @@ __device__ __forceinline__ void betti_reduce_body(const BettiLaunch& bl, const W
         if (ok && bl.retried && lane == 0) atomicAdd(bl.retried, 1u);
     }
 }
+#ifndef DGN_WIDE_PRE_WAVES
+#define DGN_WIDE_PRE_WAVES 6  // waves per SIMD of the reduction-only (prewalked) instantiations (5 / 6 / 8: 48.9 / 51.7 / 50.4 structures/s at 10 A)
+#endif
 template <int KW, bool PRE>
-__global__ __launch_bounds__(kWave * kWideWaves) __attribute__((amdgpu_waves_per_eu(DGN_WIDE_C16_WAVES)))
+__global__ __launch_bounds__(kWave * kWideWaves) __attribute__((amdgpu_waves_per_eu(PRE ? DGN_WIDE_PRE_WAVES : DGN_WIDE_C16_WAVES)))
 void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
     if constexpr (PRE) betti_reduce_body<KW>(bl, ly);
     else betti_wide_body<KW, kC16, false>(bl, ly);
