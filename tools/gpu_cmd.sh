@@ -1,12 +1,10 @@
 # scratch driver for one gpurun call (edited per call; not used by tests or the bench)
 set -o pipefail
-O=gpurun_out/r6m
+O=gpurun_out/r6o
 mkdir -p $O
 export TMPDIR=/tmp
-for r in 1 2; do
-for v in base pw6 pw8; do
-  lib=defect-gnn-cpp_amd/lib/libdgn.so; [ $v != base ] && lib=defect-gnn-cpp_amd/lib/libdgn_$v.so
-  DGN_LIB=$lib timeout -k 10 200 python3 -u tools/betti_rc10.py 128 2 > $O/rc10_${v}_$r.txt 2>&1 || { tail -20 $O/rc10_${v}_$r.txt; exit 1; }
-  echo $v $(grep "rep 1" $O/rc10_${v}_$r.txt)
-done
-done
+timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread tests -m gpu > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
+tail -2 $O/gpu_tests.txt
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || { tail -20 $O/smoke.txt; exit 1; }
+tail -1 $O/smoke.txt
+bash profiles/collect_r06.sh $O/prof
