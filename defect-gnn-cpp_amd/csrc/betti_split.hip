@@ -8,8 +8,9 @@
 // forests. So the persistence pairs of the complex are the union of its components' pairs
 // (ripser.cpp:514-1269 applied to each component gives the same multiset), and a component of one
 // point contributes one essential dim-0 class. Complexes of any size whose components each have
-// at most kWideMaxPoints points are therefore reduced by the ordinary tiers, one sub-complex per
-// component; a single component above that stays outside the envelope (DGN_ERR_UNSUPPORTED).
+// at most kWideGiantPoints (4,096) points are therefore reduced by the ordinary tiers, one
+// sub-complex per component (components of 2,049..4,096 points on the GIANT instantiation, round 6);
+// a single larger component stays outside the envelope (DGN_ERR_UNSUPPORTED).
 //
 //   big_gram_kernel        distances of clouds above 2,048 points (the reference's Gram arithmetic,
 //                          ripser_wrapper.cpp:64-67, on the VALU: the same rounded products and sums

@@ -82,16 +82,26 @@ __device__ __forceinline__ int c2i(int x) { return x * (x - 1) / 2; }
 // and (f32 bits << 32) | ~index keys.
 // MODE: kF32 (distances as f32 bits), kC16 (u16 rank codes: 4-byte -> 2-byte matrix for
 // complexes of <= 362 points, C(362, 2) < 2^16), kBig, kHuge (above).
-constexpr int kF32 = 0, kC16 = 1, kBig = 2, kHuge = 3;
+// kGiant (2,049..kWideGiantPoints points, one connected component of a caller-given cloud or triangle):
+// 12-bit vertices, keys (code << 44) | ~index (C(4096, 4) < 2^44) with the codes of the distances
+// <= thr below 2^20 (larger codes, all above thr, clamp to kGiantCodeMax; a complex with 2^20 or more
+// distances within thr is outside the envelope); HUGE's scratch bitsets, and no min-cofacet table
+// (C(n, 3) entries): clearing marks in a bitmap, the dim-2 apparent owners decided from the matrix
+// rows as in the prewalked path
+constexpr int kF32 = 0, kC16 = 1, kBig = 2, kHuge = 3, kGiant = 4;
+constexpr uint32_t kGiantCodeMax = (1u << 20) - 1;
 template <int KW, int MODE, bool PRE = false>
 struct WideCx {
     static constexpr bool BIG = MODE == kBig;
-    static constexpr bool HUGE = MODE == kHuge;
+    static constexpr bool GIANT = MODE == kGiant;
+    static constexpr bool HUGE = MODE == kHuge || GIANT;  // bitsets in scratch, u64 packed triangles
+    static constexpr bool NOMCT = PRE || GIANT;            // no dim-2 min-cofacet table
+    using CLT = std::conditional_t<GIANT, uint64_t, uint32_t>;  // a clearing-list entry (triangle index)
     static constexpr bool CODED = MODE != kF32;
     static constexpr int kWW = KW;
-    static constexpr int VB = HUGE ? 11 : (BIG ? 10 : 9);  // bits per packed vertex
+    static constexpr int VB = GIANT ? 12 : (HUGE ? 11 : (BIG ? 10 : 9));  // bits per packed vertex
     static constexpr uint64_t VM = (1ull << VB) - 1;
-    static constexpr int KS = HUGE ? 40 : (BIG ? 36 : 32);  // key: (distance code << KS) | ~index
+    static constexpr int KS = GIANT ? 44 : (HUGE ? 40 : (BIG ? 36 : 32));  // key: (distance code << KS) | ~index
     // a packed column simplex / V entry (edge or triangle, 3 VB bits)
     using PT = std::conditional_t<HUGE, uint64_t, uint32_t>;
     static constexpr PT kNoneP = ~PT(0);
@@ -124,6 +134,7 @@ struct WideCx {
     // code and the dim-2 column list come from bl.walk; clearing marks live in a bitmap (ly.clb)
     // and the dim-2 apparent owners are decided from the matrix (lookup) -- no min-cofacet table
     static_assert(!PRE || MODE == kC16, "the walk pass covers the u16-coded complexes");
+    // NOMCT without PRE (GIANT): the kernel's own passes keep their clearing marks in the bitmap too
     const BettiLaunch& bl;
     const WideLayout& ly;
     uint64_t* adj;  // LDS [n][W]: row v = the neighbours of vertex v, W words
@@ -153,10 +164,10 @@ struct WideCx {
     __device__ float value(uint32_t dc) const { return CODED ? __uint_as_float(vals[dc]) : __uint_as_float(dc); }
     // cleared-triangle bitmap (PRE): set / test bit t
     __device__ uint32_t* clbits() const { return sp<uint32_t>(ly.clb); }
-    __device__ void clear_mark(uint32_t t) const { atomicOr(&at(clbits(), t >> 5), 1u << (t & 31)); }
+    __device__ void clear_mark(uint64_t t) const { atomicOr(clbits() + (t >> 5), 1u << (t & 31)); }
     // (the marks are L2 atomics: read past the CU's L1, which may hold a stale copy of the word)
-    __device__ bool is_cleared(uint32_t t) const {
-        return (__hip_atomic_load(&at(clbits(), t >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (t & 31)) & 1u;
+    __device__ bool is_cleared(uint64_t t) const {
+        return (__hip_atomic_load(clbits() + (t >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (t & 31)) & 1u;
     }
 
     template <class T>
@@ -217,7 +228,8 @@ struct WideCx {
                 bool e = false;
                 if (j < i) {
                     const float v = L[c2i(i) + j];
-                    const uint32_t dv = CODED ? Lc[c2i(i) + j] : __float_as_uint(v);
+                    uint32_t dv = CODED ? Lc[c2i(i) + j] : __float_as_uint(v);
+                    if (GIANT) dv = min(dv, kGiantCodeMax);  // the codes above thr saturate
                     if (MODE == kC16) {
                         D16[(int64_t)i * n + j] = (uint16_t)dv;
                         D16[(int64_t)j * n + i] = (uint16_t)dv;
@@ -237,6 +249,7 @@ struct WideCx {
             }
         }
         thrc = ~wave_min_u32(~tmax);
+        if (GIANT && thrc >= kGiantCodeMax) err |= kEPoints;  // 2^20 or more distances within thr
         // HUGE: the bitsets were built by L2 atomics; the agent-scope fence drops the CU's L1 copies
         if constexpr (HUGE) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
         wave_scratch_sync();
@@ -248,7 +261,9 @@ struct WideCx {
         float* d0s = sp<float>(ly.d0);
         uint64_t best[kWW];
         int bp[kWW];
-        uint32_t intree = lane == 0 ? 1u : 0u;  // bit t: vertex 64 t + lane is in the forest
+        // bit t: vertex 64 t + lane is in the forest (64 words for GIANT)
+        using MT = std::conditional_t<(kWW > 32), uint64_t, uint32_t>;
+        MT intree = lane == 0 ? MT(1) : MT(0);
         for (int i = lane; i < n; i += kWave) par[i] = 0xFFFF;
 #pragma unroll
         for (int t = 0; t < kWW; ++t) {
@@ -266,7 +281,7 @@ struct WideCx {
 #pragma unroll
             for (int t = 0; t < kWW; ++t) {
                 const int v = 64 * t + lane;
-                const bool out = t < W && v < n && !((intree >> t) & 1u);
+                const bool out = t < W && v < n && !((intree >> t) & MT(1));
                 if (out && best[t] < lmin) {
                     lmin = best[t];
                     lt = t;
@@ -290,12 +305,12 @@ struct WideCx {
                 }
                 if (lane == 0) par[v] = (uint16_t)u;
             }
-            if (lane == (v & 63)) intree |= 1u << (v >> 6);
+            if (lane == (v & 63)) intree |= MT(1) << (v >> 6);
             wave_lds_order();
 #pragma unroll
             for (int t = 0; t < kWW; ++t) {
                 const int w = 64 * t + lane;
-                if (t < W && w < n && !((intree >> t) & 1u) && ((aw(v, t) >> lane) & 1ull)) {
+                if (t < W && w < n && !((intree >> t) & MT(1)) && ((aw(v, t) >> lane) & 1ull)) {
                     const uint64_t k = wkey(d(v, w), v > w ? bin2(v) + w : bin2(w) + v);
                     if (k < best[t]) {
                         best[t] = k;
@@ -424,6 +439,7 @@ struct WideCx {
             bool na = false;
             uint64_t colkey = 0, best = kInfW, bestp = 0;
             PT colp = 0;
+            uint64_t clr = ~0ull;  // NOMCT: the triangle this apparent pair clears
             if (e < n_edges) {
                 const uint32_t ed = edges[e];
                 const int i = (int)(ed >> VB), j = (int)(ed & VM);
@@ -443,12 +459,25 @@ struct WideCx {
                         // apparent iff (i, j) is the F-max facet of its zero-persistence cofacet:
                         // the facets with k replacing a larger vertex must be strictly shorter
                         const bool app = found && (bk > i || hdb < dij) && (bk > j || hda < dij);
-                        if (app) at(mc_t, (uint32_t)pidx(3, bestp)) = kMcClearedW;  // clearing for dim 2
-                        else na = true;
+                        if (app) {
+                            if constexpr (NOMCT) clr = pidx(3, bestp);
+                            else at(mc_t, (uint32_t)pidx(3, bestp)) = kMcClearedW;  // clearing for dim 2
+                        } else {
+                            na = true;
+                        }
                         mc = (uint16_t)bk;
                     }
                 }
                 at(mc_e, (uint32_t)(bin2(i) + j)) = mc;
+            }
+            if constexpr (NOMCT) {  // bitmap mark + its list entry (reset after the reductions)
+                const uint64_t cbal = ballot(clr != ~0ull);
+                if (clr != ~0ull) {
+                    clear_mark(clr);
+                    const int q = ncl + mask_prefix(cbal);
+                    if (q < ly.na_cap) sp<CLT>(ly.cl_list)[q] = (CLT)clr;  // (reset: see reduce_finish)
+                }
+                ncl += __popcll(cbal);
             }
             // apparent pairs have zero persistence: nothing to emit
             na_append(0, na, nna, colkey, best, bestp, colp);
@@ -578,7 +607,8 @@ struct WideCx {
                 }
                 bool cleared = false;
                 if (fresh) {
-                    cleared = at(mc_t, (uint32_t)tidx) == kMcClearedW;
+                    if constexpr (NOMCT) cleared = is_cleared(tidx);
+                    else cleared = at(mc_t, (uint32_t)tidx) == kMcClearedW;
                     dab = d(a, b);
                     dac = d(a, c);
                     dbc = d(b, c);
@@ -587,7 +617,9 @@ struct WideCx {
                 }
                 bool done;
                 if (cleared) {
-                    at(mc_t, (uint32_t)tidx) = kMcNoneW;  // consumed: the entry leaves the complex non-cleared
+                    // consumed: the entry leaves the complex non-cleared (NOMCT: the bitmap is reset
+                    // from the clearing list after the reductions)
+                    if constexpr (!NOMCT) at(mc_t, (uint32_t)tidx) = kMcNoneW;
                     done = true;
                 } else {
                     // (diameter, k) only, as in min_cofacet: a smaller k wins only with a strictly
@@ -623,7 +655,8 @@ struct WideCx {
                             na = !app;
                             mc = (uint16_t)bk;
                         }
-                        at(mc_t, (uint32_t)tidx) = mc;
+                        if constexpr (!NOMCT) at(mc_t, (uint32_t)tidx) = mc;
+                        (void)mc;
                         colkey = wkey(ds, tidx);
                         ntau = best;
                         ntv = bestp;
@@ -665,7 +698,7 @@ struct WideCx {
                 bool cl = false;
                 if (i < cnt) {
                     const uint64_t idx = ~K[i] & ((1ull << KS) - 1);
-                    if constexpr (PRE) cl = is_cleared((uint32_t)idx);
+                    if constexpr (NOMCT) cl = is_cleared(idx);
                     else cl = at(mc_t, (uint32_t)idx) == kMcClearedW;
                     if (cl) K[i] = 0ull;
                 }
@@ -819,7 +852,7 @@ struct WideCx {
             }
         }
         const int vd = drop == 0 ? v0 : (drop == 1 ? v1 : (drop == 2 ? v2 : v3));
-        if constexpr (PRE) {
+        if constexpr (NOMCT) {
             if (dim == 2) {
                 // tau = f u {vd} with diam f = diam tau (f is its F-max facet), so vd is a
                 // zero-persistence cofacet vertex of f, and tau is f's F-minimal cofacet -- the
@@ -1089,9 +1122,9 @@ struct WideCx {
             if (dim == 1) {  // clearing: tau's column is zero in dim 2 (reset after the dim-2 sort)
                 const uint64_t ti = pidx(3, tv);
                 if (lane == 0) {
-                    if constexpr (PRE) clear_mark((uint32_t)ti);
+                    if constexpr (NOMCT) clear_mark(ti);
                     else at(sp<uint16_t>(ly.mc_t), (uint32_t)ti) = kMcClearedW;
-                    if (!PRE || ncl < ly.na_cap) sp<uint32_t>(ly.cl_list)[ncl] = (uint32_t)ti;
+                    if (!PRE || ncl < ly.na_cap) sp<CLT>(ly.cl_list)[ncl] = (CLT)ti;
                 }
                 ++ncl;
             }
@@ -1175,6 +1208,7 @@ struct WideCx {
     int nna1 = 0, nna2 = 0, base2 = 0, ncl = 0;
     __device__ void apparent(int64_t gi, int64_t slot) {
         load(gi, slot);
+        if (GIANT && err) return;  // outside the envelope: NaN outputs and the flag (finish)
         if constexpr (PRE) {
             apparent_from_walk(slot);
             return;
@@ -1252,8 +1286,11 @@ struct WideCx {
         if (err == 0u) reduce(2, nna2, base2);
         // the dim-1 clearing marks were read by the dim-2 sort; reset them for the next complex
         // (every other min-cofacet entry a later complex reads is rewritten by its dim-2 pass)
-        const uint32_t* cl = sp<uint32_t>(ly.cl_list);
-        if constexpr (PRE) {
+        const CLT* cl = sp<CLT>(ly.cl_list);
+        if constexpr (GIANT) {
+            // every set bit of the bitmap is listed (ncl <= the edges < 2^20 <= na_cap)
+            for (int i = lane_id(); i < ncl && i < ly.na_cap; i += kWave) clbits()[cl[i] >> 5] = 0u;
+        } else if constexpr (PRE) {
             // every set bit of the bitmap is listed (a word shared by two entries is zeroed twice)
             const int64_t words = ((int64_t)c2i(n) * (n - 2) / 3 + 31) / 32 + 1;
             const int ncw = (int)uniw(bl.walk.meta[8 * wslot + kWmCl]);
@@ -1284,7 +1321,7 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
     // alone while the other wave loads its next complex: twice the waves per CU for the LDS of one
     // complex (the reductions, about half of a 10 A complex's time, read no LDS).
     extern __shared__ uint64_t wide_lds[];
-    constexpr bool kHugeMode = MODE == kHuge;
+    constexpr bool kHugeMode = MODE == kHuge || MODE == kGiant;
     const int64_t ww = (ly.nmax + 63) / 64;
     const int lane = lane_id();
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
@@ -1810,7 +1847,8 @@ WideKernel wide_kernel_for(int nmax, bool c16, bool pre = false) {
     if (w <= 6) return betti_wide_kernel<6, kF32>;
     if (w <= 8) return betti_wide_kernel<8, kF32>;
     if (w <= 16) return betti_wide_kernel<16, kBig>;  // 513..1024 points: rank-coded distances (BIG)
-    return betti_wide_kernel<32, kHuge>;              // 1025..2048 points: HUGE
+    if (w <= 32) return betti_wide_kernel<32, kHuge>; // 1025..2048 points: HUGE
+    return betti_wide_kernel<64, kGiant>;             // 2049..4096 points (caller-given clouds): GIANT
 }
 
 size_t wide_lds_bytes(int nmax, bool pre = false) {  // per workgroup: token, adjacency, parents
@@ -1834,6 +1872,7 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
     const int64_t n = nmax;
     const int64_t e = n * (n - 1) / 2, t = n * (n - 1) * (n - 2) / 6;
     const bool huge = nmax > kWideBigPoints;
+    const bool giant = nmax > kWideMaxPoints;  // no dim-2 min-cofacet table: a clearing bitmap
     const int64_t pt = huge ? 8 : 4;  // bytes of a packed column simplex (HUGE: 33-bit triangles)
     int64_t cap_max = big ? (int64_t(1) << (base_log2 + 2 * grow)) : (int64_t(1) << 17);
     // the pivot hash holds 2 cap entries and is probed with 32-bit masks: columns stop at 2^29
@@ -1861,15 +1900,15 @@ WideLayout betti_wide_layout(int nmax, bool big, int64_t cap_limit, int grow, in
     l.prewalked = prewalked ? 1 : 0;
     l.D = take(prewalked ? 0 : 4 * n * n);  // prewalked: the walk pass's per-complex matrix
     l.mc_e = take(prewalked ? 0 : 2 * e);   // prewalked: the walk pass's per-complex table
-    l.mc_t = take(prewalked ? 0 : 2 * t);   // prewalked: no dim-2 min-cofacet table
-    l.clb = take(prewalked ? 4 * (t / 32 + 2) : 0);
+    l.mc_t = take(prewalked || giant ? 0 : 2 * t);   // prewalked / giant: no dim-2 min-cofacet table
+    l.clb = take(prewalked || giant ? 4 * (t / 32 + 2) : 0);
     l.edges = take(prewalked ? 0 : 4 * e);
     l.adj = take(huge ? 8 * n * ((n + 63) / 64) : 0);
     l.na_key = take(8 * cap);
     l.na_tau = take(8 * cap);
     l.na_tv = take(8 * cap);
     l.na_col = take(pt * cap);
-    l.cl_list = take(4 * cap);  // triangle indices of the dim-1 clearing marks
+    l.cl_list = take((giant ? 8 : 4) * cap);  // triangle indices of the dim-1 clearing marks
     l.vstore = take(pt * (int64_t)l.vs_cap);
     l.vlist = take(pt * (int64_t)l.vl_cap);
     l.h_key = take(8 * 2 * cap);
@@ -1887,7 +1926,7 @@ hipError_t betti_wide_init_scratch(hipStream_t s, const WideLayout& l, int waves
     if (e != hipSuccess) return e;
     // mc_e and mc_t (with their alignment padding) lie between l.mc_e and l.clb
     if (l.clb > l.mc_e) e = hipMemset2DAsync(l.base + l.mc_e, (size_t)l.total, 0xFF, (size_t)(l.clb - l.mc_e), (size_t)waves, s);
-    if (e != hipSuccess || !l.prewalked) return e;
+    if (e != hipSuccess || l.edges == l.clb) return e;  // the clearing bitmap (prewalked / giant) starts empty
     return hipMemset2DAsync(l.base + l.clb, (size_t)l.total, 0, (size_t)(l.edges - l.clb), (size_t)waves, s);
 }
 

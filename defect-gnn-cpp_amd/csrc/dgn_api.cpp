@@ -457,10 +457,13 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
         }
         max_points = (int)nw().max_candidates + 1;
     }
-    if (max_points > betti_max_points())
+    // caller-given triangles (one connected component at a time, dgn_host_persistence's split) reach
+    // the GIANT instantiation; clouds and atom-centred complexes stop at the distance kernels' 2,048
+    const int envelope = lower ? kWideGiantPoints : betti_max_points();
+    if (max_points > envelope)
         return fail(c, DGN_ERR_UNSUPPORTED,
                     "local complex with " + std::to_string(max_points) + " points exceeds the " +
-                        std::to_string(betti_max_points()) + "-point kernel envelope (see DESIGN.md)");
+                        std::to_string(envelope) + "-point kernel envelope (see DESIGN.md)");
     // scratch slots: the main grid's plus kOverflowWaves for the forked overflow tier
     constexpr int kOverflowWaves = 512;
     if (c->betti_slots == 0) c->betti_slots = betti_grid_waves(c->device) + kOverflowWaves;
@@ -769,7 +772,11 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
             WideLayout big = betti_wide_layout(nmax, true, 0, grow, c->dbg_big_log2 ? c->dbg_big_log2 : 24);
             size_t free_b = 0, total_b = 0;
             if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
-            const int64_t slice = coded ? std::min<int64_t>(nretry, 512) : nretry;
+            // (GIANT: 8.4 M distances per 4,096-point complex; a slice keeps its codes below 16 GB and
+            // its segmented-sort offsets in int32)
+            const int64_t slice = coded ? std::max<int64_t>(1, std::min<int64_t>({nretry, 512, INT32_MAX / rstride,
+                                                                                   (int64_t(16) << 30) / (8 * rstride)}))
+                                        : nretry;
             const int64_t nsl = (nretry + slice - 1) / slice;
             const size_t rank_bytes = coded ? betti_rank_temp_bytes(slice, rstride) + 8 * (size_t)slice * rstride : 0;
             const int64_t budget =
@@ -1032,7 +1039,7 @@ int dgn_debug_check_wide_layouts(int64_t* first_bad) {
     if (!first_bad) return DGN_ERR_ARG;
     *first_bad = -1;
     auto pow2 = [](int64_t x) { return x > 0 && x <= INT32_MAX && (x & (x - 1)) == 0; };
-    for (int nmax = 65; nmax <= betti_max_points(); ++nmax)
+    for (int nmax = 65; nmax <= kWideGiantPoints; ++nmax)
         for (int big = 0; big <= 1; ++big)
             for (int grow = 0; grow <= (big ? kWideMaxGrow : 0); ++grow) {
                 const WideLayout l = betti_wide_layout(nmax, big != 0, 0, grow);
@@ -1388,7 +1395,8 @@ int dgn_debug_betti_clouds(dgn_ctx* c, const dgn_batch* h, double rc, int64_t fi
 // (ripser.cpp:386-395, 514-1269 on a block-diagonal coboundary matrix); each component of two or
 // more points is reduced by the ordinary Betti pass as a caller-given triangle, a one-point
 // component adds one essential dim-0 class. pairs [C][3][cap][2] (unsorted here) and kk [C][4] are
-// filled on the host. A component above kWideMaxPoints points: DGN_ERR_UNSUPPORTED.
+// filled on the host. A component above kWideGiantPoints points (or a GIANT one with 2^20 or more
+// distances within the threshold): DGN_ERR_UNSUPPORTED.
 static int persistence_split(dgn_ctx* c, const double* d_clouds, const float* d_lower, const int32_t* d_np,
                              const int32_t* npoints, int64_t C, int32_t max_points, double threshold, float* pairs,
                              int32_t cap, std::vector<int32_t>& kk) {
@@ -1425,10 +1433,10 @@ static int persistence_split(dgn_ctx* c, const double* d_clouds, const float* d_
                     ++kk[4 * (size_t)(c0 + i) + 1];  // one point: an essential dim-0 class, no pairs
                     continue;
                 }
-                if (count[(size_t)r] > kWideMaxPoints)
+                if (count[(size_t)r] > kWideGiantPoints)
                     return fail(c, DGN_ERR_UNSUPPORTED,
                                 "a connected component of " + std::to_string(count[(size_t)r]) +
-                                    " points at this threshold exceeds the " + std::to_string(kWideMaxPoints) +
+                                    " points at this threshold exceeds the " + std::to_string(kWideGiantPoints) +
                                     "-point kernel envelope (see DESIGN.md)");
                 first[(size_t)r] = (int64_t)map.size();
                 off.push_back((int64_t)map.size());

@@ -178,6 +178,10 @@ struct BettiLaunch {
 // kWideBigPoints, 11-bit vertices and the adjacency in scratch above) in the retry launch after
 // betti_rank_codes
 constexpr int kWideMaxPoints = 2048;
+// caller-given clouds / triangles (dgn_host_persistence[_lower], one connected component at a time):
+// complexes of up to this many points whose distances within the threshold number below 2^20 (the
+// GIANT instantiation, betti_wide.hip)
+constexpr int kWideGiantPoints = 4096;
 // dgn_host_persistence[_lower] above kWideMaxPoints points: split into the connected components of
 // the threshold graph (betti_split.hip), each reduced by the ordinary tiers; the union-find keeps
 // a complex's parents in LDS (4 B per point)

@@ -366,15 +366,67 @@ def test_split_many_small_components_beside_a_large_one(ctx):
             assert np.array_equal(pl[c, di, :counts[c, col]], pairs[c, di, :counts[c, col]]), (c, di)
 
 
+def _tube(rng, n, ds, radius):
+    """n points in a tube of the given radius around a slowly turning random walk of step ds: one
+    connected component at threshold 1 with a few thousand 1- and 2-cycles."""
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    for i in range(1, n):
+        d[i] = 0.97 * d[i - 1] + 0.03 * d[i]
+        d[i] /= np.linalg.norm(d[i])
+    c = np.cumsum(d * ds, axis=0)
+    off = rng.normal(size=(n, 3))
+    off -= (off * d).sum(1, keepdims=True) * d
+    off /= np.linalg.norm(off, axis=1, keepdims=True)
+    return c + off * radius * np.sqrt(rng.uniform(0, 1, (n, 1)))
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="verbatim Ripser (oracle/_ref) not built")
+def test_single_component_above_2048_points(ctx):
+    """One connected component of 2,100..3,000 points (dgn_host_persistence / _lower): the GIANT
+    instantiation (12-bit vertices, keys (code << 44) | ~index, no min-cofacet table), against
+    verbatim Ripser on the whole cloud (ripser.cpp:154, 514-1269 have no point cap)."""
+    rng = np.random.default_rng(61)
+    specs = [(2100, 0.12, 0.6), (2600, 0.1, 0.7), (3000, 0.15, 0.6)]
+    npts = np.array([n for n, _, _ in specs], np.int32)
+    clouds = np.zeros((len(specs), npts.max(), 3))
+    for c, (n, ds, rad) in enumerate(specs):
+        clouds[c, :n] = _tube(rng, n, ds, rad)
+    thr = 1.0
+    pairs, counts = ctx.host_persistence(clouds, npts, thr, cap=4096)
+    lows = []
+    for c, n in enumerate(npts):
+        low = O.local_distances(clouds[c, :n])
+        lows.append(low)
+        r = O.ref_persistence(low, int(n), np.float32(thr))
+        assert r["n_inf0"] == 1 and counts[c, 1] == 1, c  # a single component
+        for di, d in enumerate(("dim0", "dim1", "dim2")):
+            assert np.array_equal(pairs[c, di, :counts[c, [0, 2, 3][di]]], r[d]), (c, n, d)
+    m = int(npts.max())
+    L = np.zeros((len(specs), m * (m - 1) // 2), np.float32)
+    for c, low in enumerate(lows):
+        L[c, :low.shape[0]] = low
+    pl, cl = ctx.host_persistence_lower(L, npts, m, thr, cap=4096)
+    assert np.array_equal(cl, counts)
+    for c in range(len(specs)):
+        for di, col in enumerate((0, 2, 3)):
+            assert np.array_equal(pl[c, di, :cl[c, col]], pairs[c, di, :counts[c, col]])
+
+
 def test_above_2048_points_fails_loudly(ctx):
     # outside the envelope (DESIGN.md §8): an explicit DGN_ERR_UNSUPPORTED, never a silent or
-    # truncated result -- a caller-given 2,100-point cloud whose threshold graph is one connected
-    # component (every point within the threshold of its neighbours), and FCC-256 at 21 A
-    # (~3,100-point local complexes, the count pass finds them before any Betti launch)
+    # truncated result -- one connected component above 4,096 points; a 2,100-point component whose
+    # distances within the threshold number 2^20 or more (every pair: the GIANT keys hold codes below
+    # 2^20); and FCC-256 at 21 A (~3,100-point atom-centred complexes, above the distance search's
+    # 2,048 candidates: the count pass finds them before any Betti launch)
     rng = np.random.default_rng(5)
-    cloud = rng.uniform(0.0, 12.0, size=(1, 2100, 3))
+    cloud = _tube(rng, 4200, 0.12, 0.6)[None]
     with pytest.raises(dgn.DgnError) as e:
-        ctx.host_persistence(cloud, np.array([2100], np.int32), 3.0)
+        ctx.host_persistence(cloud, np.array([4200], np.int32), 1.0)
+    assert e.value.status == 5
+    dense = rng.uniform(0.0, 1.0, size=(1, 2100, 3))
+    with pytest.raises(dgn.DgnError) as e:
+        ctx.host_persistence(dense, np.array([2100], np.int32), 3.0)
     assert e.value.status == 5
     with pytest.raises(dgn.DgnError) as e:
         ctx.host_betti(dgn.synth_batch("fcc", 4, 1), 21.0)
