@@ -91,7 +91,7 @@ int dgn_debug_retry_count(dgn_ctx* ctx, int64_t* count);
  * (no synchronization itself; tests of the asynchronous device entry points). */
 int dgn_debug_host_syncs(dgn_ctx* ctx, int64_t* count);
 /* Diagnostics (host arithmetic only, no device, no context): every wide-kernel scratch layout the
- * Betti pass can choose (65..2,048 points, regular and capacity-retry at every growth level) has
+ * Betti pass can choose (65..4,096 points, regular and capacity-retry at every growth level) has
  * positive power-of-two int32 table capacities. DGN_OK, or DGN_ERR_INTERNAL with *first_bad =
  * nmax * 64 + big * 16 + grow of the first layout that does not. */
 int dgn_debug_check_wide_layouts(int64_t* first_bad);
@@ -257,7 +257,10 @@ void dgn_edge_arrays_free(dgn_edge_arrays* a);
 
 /* Local-complex persistence from point clouds (replaces topology::compute_persistence,
  * src/topology/ripser_wrapper.cpp:60-70). clouds: [C][max_points][3] f64 (host), npoints[C].
- * pairs: [C][3][cap][2] f32 (host) sorted ascending by (birth, death); counts [C][4]. */
+ * pairs: [C][3][cap][2] f32 (host) sorted ascending by (birth, death); counts [C][4].
+ * Envelope: max_points <= 16,384; clouds above 2,048 points are reduced per connected component of
+ * their threshold graph, each of at most 4,096 points and, above 2,048, fewer than 2^20 distances
+ * within the threshold; outside it DGN_ERR_UNSUPPORTED, never a truncated result. */
 int dgn_host_persistence(dgn_ctx* ctx, const double* clouds, const int32_t* npoints, int64_t num_clouds,
                          int32_t max_points, double threshold, float* pairs, int32_t cap, int32_t* counts);
 
