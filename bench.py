@@ -94,7 +94,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     # one process per GPU; ranks beyond the visible devices share them (gloo tests on one GPU)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    # under torch.distributed.run (WORLD_SIZE set, the driver's N > 1 launches) the timing barrier and
+    # the max-over-ranks reduction go through the process group, even for one rank
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -132,17 +135,17 @@ def main():
     ctx.enable_timing(True)
 
     # ---- timed region: barrier + sync on both sides, max over ranks ----
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -224,7 +227,7 @@ def main():
         result["side"] = side_lines(dgn, abi, ctx, dev, args, torch)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -52,3 +52,21 @@ def test_bench_two_ranks_gloo(tmp_path, ctx):
         assert np.array_equal(np.load(tmp_path / f"rank{rank}_row_ptr.npy"), g["row_ptr"]), rank
         assert np.array_equal(np.load(tmp_path / f"rank{rank}_col.npy"), g["col"]), rank
         assert np.array_equal(np.load(tmp_path / f"rank{rank}_dist.npy"), g["dist"]), rank
+
+
+def test_bench_one_rank_nccl(tmp_path):
+    """The launcher path the 8-GPU driver run takes -- torch.distributed.run with the default nccl
+    (RCCL) backend for the timing barrier and the max-over-ranks reduction -- on the one GPU this box
+    has (one rank: RCCL needs a device per rank). The line reports n_gpus 1 and the rank's value."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--structures", str(B), "--steps", "2", "--warmup", "1", "--no-side", "--no-cpu-baseline",
+           "--no-alt-rbf", "--dump-shards", str(tmp_path)]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 1 and j["value"] > 0 and j["config"]["structures_per_gpu"] == B
+    assert (tmp_path / "rank0_counts.npy").exists()
