@@ -157,6 +157,7 @@ struct WideCx {
     uint32_t thrc = 0;
 
     const uint8_t* dm = nullptr;  // the distance matrix: this wave's scratch (ly.D) or PRE the walk pass's
+    int ns = 0;                   // its row stride in elements (n; PRE: n rounded up to 4, 8-byte rows)
     int64_t wslot = 0;            // the complex's slice position (PRE: its walk-pass outputs)
     uint16_t* mce = nullptr;      // dim-1 min-cofacet table: scratch (ly.mc_e) or PRE the walk pass's
     float* d0p = nullptr;         // dim-0 deaths: scratch (ly.d0) or PRE the walk pass's
@@ -175,14 +176,14 @@ struct WideCx {
     // d(i, j) at a per-lane (i, j): scalar matrix base + 32-bit element offset (i n + j < 2^22), not
     // a 64-bit vector address built from a 64-bit product per read
     __device__ uint32_t d(int i, int j) const {
-        const uint32_t ix = (uint32_t)i * (uint32_t)n + (uint32_t)j;
+        const uint32_t ix = (uint32_t)i * (uint32_t)ns + (uint32_t)j;
         if (MODE == kC16) return at(reinterpret_cast<const uint16_t*>(dm), ix);
         return at(reinterpret_cast<const uint32_t*>(dm), ix);
     }
     __device__ uint64_t aw(int v, int w) const { return adj[v * W + w]; }
     // d(a, x) for a wave-uniform row a: scalar row base + 32-bit lane offset
     __device__ uint32_t drow(int a, uint32_t x) const {
-        const uint32_t ra = (uint32_t)a * (uint32_t)n;
+        const uint32_t ra = (uint32_t)a * (uint32_t)ns;
         if (MODE == kC16) return at(reinterpret_cast<const uint16_t*>(dm) + ra, x);
         return at(reinterpret_cast<const uint32_t*>(dm) + ra, x);
     }
@@ -867,20 +868,31 @@ struct WideCx {
                 const uint32_t fd = kdiam(bestk);
                 const int t0 = vd >> 6;
                 uint32_t ra[KW], rb[KW], rc[KW];
-#pragma unroll
-                for (int t = 0; t < KW; ++t) {
-                    if (t < t0 || t >= W) continue;
-                    const uint32_t x = (uint32_t)min(64 * t + lane, n - 1);
-                    ra[t] = drow(fa, x);
-                    rb[t] = drow(fb, x);
-                    rc[t] = drow(fc, x);
-                }
                 bool later = false;
+                if constexpr (PRE) {  // 8-byte rows: packed vectors (prow)
+                    prow(fa, ra);
+                    prow(fb, rb);
+                    prow(fc, rc);
 #pragma unroll
-                for (int t = 0; t < KW; ++t) {
-                    if (t < t0 || t >= W) continue;
-                    const int x = 64 * t + lane;
-                    later |= x > vd && x < n && max(max(ra[t], rb[t]), rc[t]) <= fd;
+                    for (int t = 0; t < KW; ++t) {
+                        const int x = slot_x(t, lane);
+                        later |= x > vd && x < n && max(max(ra[t], rb[t]), rc[t]) <= fd;
+                    }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < KW; ++t) {
+                        if (t < t0 || t >= W) continue;
+                        const uint32_t x = (uint32_t)min(64 * t + lane, n - 1);
+                        ra[t] = drow(fa, x);
+                        rb[t] = drow(fb, x);
+                        rc[t] = drow(fc, x);
+                    }
+#pragma unroll
+                    for (int t = 0; t < KW; ++t) {
+                        if (t < t0 || t >= W) continue;
+                        const int x = 64 * t + lane;
+                        later |= x > vd && x < n && max(max(ra[t], rb[t]), rc[t]) <= fd;
+                    }
                 }
                 if (!ballot(later)) app = (PT)bestf;
                 return kNoMetaW;
@@ -943,6 +955,34 @@ struct WideCx {
         return true;
     }
 
+    // PRE rows as packed u16 vectors (row stride ns, a multiple of 4): KW 2 -- one dword per lane,
+    // vertices 2k, 2k + 1; KW 4 -- one dwordx2, 4k .. 4k + 3; KW 6 -- a dwordx2 (4k .. 4k + 3) and a
+    // dword (256 + 2k, 256 + 2k + 1). Lanes past n read the next row or the complex's padding.
+    __device__ static int slot_x(int t, int k) {
+        if constexpr (KW == 2) return 2 * k + t;
+        else if constexpr (KW == 4) return 4 * k + t;
+        else return t < 4 ? 4 * k + t : 256 + 2 * k + (t - 4);
+    }
+    __device__ void prow(int a, uint32_t (&out)[KW]) const {
+        static_assert(!PRE || KW == 2 || KW == 4 || KW == 6, "prewalked instantiations: 2, 4, 6 words");
+        const int k = lane_id();
+        const uint16_t* R = reinterpret_cast<const uint16_t*>(dm) + (uint32_t)a * (uint32_t)ns;
+        if constexpr (KW == 2) {
+            const uint32_t w = at(reinterpret_cast<const uint32_t*>(R), (uint32_t)k);
+            out[0] = w & 0xFFFFu;
+            out[1] = w >> 16;
+        } else {
+            const uint64_t w = at(reinterpret_cast<const uint64_t*>(R), (uint32_t)k);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) out[q] = (uint32_t)(w >> (16 * q)) & 0xFFFFu;
+            if constexpr (KW == 6) {
+                const uint32_t w2 = at(reinterpret_cast<const uint32_t*>(R), 128u + (uint32_t)k);
+                out[4] = w2 & 0xFFFFu;
+                out[5] = w2 >> 16;
+            }
+        }
+    }
+
     // Pivot of sum(delta s, s in V) above `floor` (the previous pivot): lane k evaluates the
     // cofacets s u {x}, x = 64 t + k; a cofacet arises once per facet in V; the multiplicity of
     // the minimum is summed over lanes (a lane can meet it from several words). Even: raise the
@@ -964,6 +1004,16 @@ struct WideCx {
                 const int c = pv(s, 0);
                 // every word's row reads issued before any is used (coalesced rows a, b, c)
                 uint32_t da[KW], db[KW], dc[KW];
+                if constexpr (PRE) {
+                    // PRE (8-byte rows): packed u16 vectors, slot t of lane k is vertex slot_x(t, k)
+                    // -- a third of the per-word u16 loads
+                    prow(a, da);
+                    prow(b, db);
+                    if (dim == 2) prow(c, dc);
+                    else
+#pragma unroll
+                        for (int t = 0; t < KW; ++t) dc[t] = 0u;
+                } else
 #pragma unroll
                 for (int t = 0; t < KW; ++t) {
                     const int x = min(64 * t + k, n - 1);
@@ -979,8 +1029,8 @@ struct WideCx {
                 }
 #pragma unroll
                 for (int t = 0; t < KW; ++t) {
-                    if (t >= W) break;
-                    const int x = 64 * t + k;
+                    if (!PRE && t >= W) break;
+                    const int x = PRE ? slot_x(t, k) : 64 * t + k;
                     const uint32_t dd = max(max(ds, dc[t]), max(da[t], db[t]));
                     const uint64_t p = pinsert(dim + 1, s, x);
                     const uint64_t kk = PACKKEY ? pkey(dd, p) : wkey(dd, pidx(dim + 2, p));
@@ -1354,6 +1404,7 @@ __device__ __forceinline__ void betti_wide_body(const BettiLaunch& bl, const Wid
             if (MODE != kF32) cx.vals = bl.rank_sorted + wi * bl.rank_stride;
             cx.wslot = wi;
             cx.dm = scr + ly.D;
+            cx.ns = n;
             cx.mce = reinterpret_cast<uint16_t*>(scr + ly.mc_e);
             cx.d0p = reinterpret_cast<float*>(scr + ly.d0);
             // take the buffer: every lane tries the same compare-and-swap, the wave holds it when one
@@ -1408,6 +1459,7 @@ __device__ __forceinline__ void betti_reduce_body(const BettiLaunch& bl, const W
         cx.vals = bl.rank_sorted + wi * bl.rank_stride;
         cx.wslot = wi;
         cx.dm = reinterpret_cast<const uint8_t*>(bl.walk.dmat + wi * bl.walk.dstride);
+        cx.ns = (n + 3) & ~3;
         cx.mce = bl.walk.mce + wi * bl.walk.mstride;
         cx.d0p = bl.walk.d0 + wi * bl.walk.d0stride;
         cx.apparent(gi, wi);
@@ -1589,10 +1641,11 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
         }
     } else {
         uint16_t* D = wo.dmat + wi * wo.dstride;
+        const int ns = (n + 3) & ~3;  // 8-byte rows (the reductions read them as packed vectors)
         for (int i = wv - 1; i < n; i += kWalkWaves - 1) {
             const int ci = c2i(i);
-            for (int x = lane; x < n; x += kWave)
-                D[i * n + x] = x == i ? (uint16_t)0xFFFF : (x < i ? T[ci + x] : T[c2i(x) + i]);
+            for (int x = lane; x < ns; x += kWave)
+                D[i * ns + x] = x == i || x >= n ? (uint16_t)0xFFFF : (x < i ? T[ci + x] : T[c2i(x) + i]);
         }
     }
     __syncthreads();  // the forest (is a dim-1 column a tree edge?)
@@ -1945,7 +1998,8 @@ int betti_wide_resident_waves(int device, int nmax, bool c16, bool pre) {
 WalkOut betti_walk_out_layout(int nmax) {
     WalkOut w{};
     w.nmax = nmax;
-    w.dstride = ((int64_t)nmax * nmax + 127) / 128 * 128;          // u16
+    // u16, rows of (n + 3) & ~3 elements, + 512 of padding for the packed reads past the last row
+    w.dstride = ((int64_t)nmax * ((nmax + 3) & ~3) + 512 + 127) / 128 * 128;
     w.d0stride = ((int64_t)nmax + 63) / 64 * 64;                   // f32
     w.mstride = ((int64_t)nmax * (nmax - 1) / 2 + 127) / 128 * 128;  // u16
     w.cap1 = kWalkCap;
