@@ -1468,7 +1468,7 @@ __device__ __forceinline__ void betti_reduce_body(const BettiLaunch& bl, const W
     }
 }
 #ifndef DGN_WIDE_PRE_WAVES
-#define DGN_WIDE_PRE_WAVES 6  // waves per SIMD of the reduction-only (prewalked) instantiations (5 / 6 / 8: 48.9 / 51.7 / 50.4 structures/s at 10 A)
+#define DGN_WIDE_PRE_WAVES 8  // waves per SIMD of the reduction-only (prewalked) instantiations (A/B at 10 A, 128 structures: 5 / 6 / 8 = 48.9 / 51.7 / 50.4; with packed rows 6 / 7 / 8 = 53.6-53.9 / 53.3-54.0 / 55.2-55.4 structures/s)
 #endif
 template <int KW, bool PRE>
 __global__ __launch_bounds__(kWave * kWideWaves) __attribute__((amdgpu_waves_per_eu(PRE ? DGN_WIDE_PRE_WAVES : DGN_WIDE_C16_WAVES)))
