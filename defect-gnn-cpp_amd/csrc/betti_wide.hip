@@ -1493,6 +1493,9 @@ void betti_wide_kernel_c16(BettiLaunch bl, WideLayout ly) {
 // are dropped when the reduction kernel reads the list). No dim-2 min-cofacet table: the reduction
 // decides apparent owners from the matrix (lookup, PRE form).
 constexpr int kWalkWaves = 16;
+#ifndef DGN_WALK_STEP
+#define DGN_WALK_STEP 4  // candidates per step of the walk pass's dim-2 walk
+#endif
 constexpr int kWalkRing = 128;  // queued triangles per wave (refilled below 64: at most 63 + 64 held)
 __device__ __forceinline__ uint32_t c2u(int x) { return ((uint32_t)x * (uint32_t)(x - 1)) >> 1; }
 __device__ __forceinline__ uint32_t walk_ticket(uint32_t* ctr) {  // wave-uniform, no branch on the lane
@@ -1813,7 +1816,7 @@ __global__ __launch_bounds__(kWave * kWalkWaves) void betti_walk_kernel(BettiLau
                 m = aw(ea, w) & aw(eb, w) & aw(c, w);
             }
             // up to kS candidates of this word, highest first
-            constexpr int kS = 4;
+            constexpr int kS = DGN_WALK_STEP;
             int kk[kS];
             bool val[kS];
 #pragma unroll
