@@ -140,26 +140,12 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
-// lanes [0, m) as a mask (m wave-uniform: scalar code). ballot(cmp) & lanes_below(m) keeps a
-// ballot to one v_cmp, where ballot(lane < m && cmp) materializes the combined bool first.
-#ifndef DGN_SALU_V1
-#define DGN_SALU_V1 0
-#endif
-#ifndef DGN_SALU_V2
-#define DGN_SALU_V2 0
-#endif
-#ifndef DGN_SALU_V3
-#define DGN_SALU_V3 0
-#endif
-#ifndef DGN_SALU_V4
-#define DGN_SALU_V4 0
-#endif
+// lanes [0, m) as a mask (full EXEC): one v_cmp into an SGPR pair. The narrow kernel is bound by
+// the scalar unit's issue rate (one SALU per SIMD every ~4 cycles against a VALU every ~2.4 at 8
+// waves per SIMD, tools/ubench/issue.hip), so masks and per-entry arithmetic go to the VALU where
+// the scalar form would take several SALU (the shift/select form of this mask: 5-6).
 __device__ __forceinline__ uint64_t lanes_below(int m) {
-#if DGN_SALU_V1
     return __builtin_amdgcn_ballot_w64((int)(threadIdx.x & 63) < m);
-#else
-    return m >= 64 ? ~0ull : (m <= 0 ? 0ull : (1ull << m) - 1ull);
-#endif
 }
 __device__ __forceinline__ int c2(int x) { return x * (x - 1) / 2; }
 __device__ __forceinline__ int c3(int x) { return x * (x - 1) * (x - 2) / 6; }
@@ -347,7 +333,6 @@ struct Complex {
     // F-minimal cofacet (recorded for every column by the lane-parallel pass; tree edges and
     // cleared triangles hold kNone), else kNone.
     __device__ uint32_t apparent_owner_wave(int dim, uint64_t tau) const {
-#if DGN_SALU_V4
         // computed redundantly by every lane on the VALU (the scalar unit is the bound port)
         uint32_t th, tl;
         asm("v_mov_b32 %0, %1" : "=v"(th) : "s"((uint32_t)(tau >> 32)));
@@ -357,7 +342,6 @@ struct Complex {
         const uint32_t vm = at(mincof_of(dim), dim == 1 ? col_dense(1, vf)
                                                          : tri_dense_lane((vf >> 16) & 255, (vf >> 8) & 255, vf & 255));
         return uni(vm == extra_vertex(key_packed(vt), vf) ? vf : kNone);
-#endif
         const uint32_t f = uni(max_facet(dim, uni64(tau)));
         const uint32_t m = at(mincof_of(dim), col_dense(dim, f));
         return uni(m) == extra_vertex(key_packed(tau), f) ? f : kNone;
@@ -395,7 +379,6 @@ struct Complex {
     }
     __device__ void piv_push(int i, uint64_t tau, uint32_t meta) {
         const int lane = lane_id();
-#if DGN_SALU_V2
         if (i < 2 * kWave) {
             const bool w0 = lane == i, w1 = lane == i - kWave;
             pk0 = w0 ? tau : pk0;
@@ -403,13 +386,6 @@ struct Complex {
             pk1 = w1 ? tau : pk1;
             pm1 = w1 ? meta : pm1;
         } else if (lane == 0) {
-#else
-        if (i < kWave) {
-            if (lane == i) { pk0 = tau; pm0 = meta; }
-        } else if (i < 2 * kWave) {
-            if (lane == i - kWave) { pk1 = tau; pm1 = meta; }
-        } else if (lane == 0) {
-#endif
             sp<uint64_t>(ScratchLayout::piv)[i] = tau;
             at(sp<uint32_t>(ScratchLayout::vmeta), i) = meta;
         }
@@ -427,16 +403,8 @@ struct Complex {
     }
     __device__ void v_set(int i, uint32_t sp_) {
         const int lane = lane_id();
-#if DGN_SALU_V2
         vs0 = lane == i ? sp_ : vs0;
         vs1 = lane == i - 64 ? sp_ : vs1;
-#else
-        if (i < 64) {
-            if (lane == i) vs0 = sp_;
-        } else if (lane == i - 64) {
-            vs1 = sp_;
-        }
-#endif
     }
     __device__ int v_find(uint32_t x, int v) const {
         uint64_t bal = ballot(vs0 == x) & lanes_below(v);
@@ -478,7 +446,6 @@ struct Complex {
     // complemented vertex byte (kc = 255 - k, perm byte 4), with the byte order picked by where k
     // falls among the vertices of s (selector table kSel*). Branch-free: v_cndmask only.
     __device__ uint64_t cofacet_key(int dim, int k, uint32_t kc, uint32_t sp_, uint32_t ds) const {
-#if DGN_SALU_V3
         // the entry's row offsets and complement on the VALU (the scalar unit is the bound port)
         uint32_t vsp;
         asm("v_mov_b32 %0, %1" : "=v"(vsp) : "s"(sp_));
@@ -498,25 +465,6 @@ struct Complex {
         }
         const uint32_t nk = __builtin_amdgcn_perm(kc, ~vsp, sel);
         return ((uint64_t)dd << 32) | (uint64_t)nk;
-#else
-        const int a = dim == 1 ? (int)((sp_ >> 8) & 255) : (int)((sp_ >> 16) & 255);
-        const int b = dim == 1 ? (int)(sp_ & 255) : (int)((sp_ >> 8) & 255);
-        const int c = (int)(sp_ & 255);
-        // lane k reads row entries (x, k): consecutive lanes, consecutive banks
-        // (u32 operands throughout: a u32 / u16 max resolves to the double overload, three f64
-        // conversions and a v_max_f64 per cofacet)
-        uint32_t dd = max(ds, max((uint32_t)Db()[a * S + k], (uint32_t)Db()[b * S + k]));
-        uint32_t sel;
-        if (dim == 1) {
-            // ~(k,a,b) / ~(a,k,b) / ~(a,b,k); the top byte of ~pack3 is 0xFF (S1 byte 2 of ~sp_)
-            sel = k > a ? 0x02040100u : (k > b ? 0x02010400u : 0x02010004u);
-        } else {
-            dd = max(dd, (uint32_t)Db()[c * S + k]);
-            sel = k > a ? 0x04020100u : (k > b ? 0x02040100u : (k > c ? 0x02010400u : 0x02010004u));
-        }
-        const uint32_t nk = __builtin_amdgcn_perm(kc, ~sp_, sel);
-        return ((uint64_t)dd << 32) | (uint64_t)nk;
-#endif
     }
 
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
