@@ -66,7 +66,7 @@ def main():
           "per_complex": per,
           "note": ("walk = betti_walk_kernel (one 1,024-thread workgroup per complex: the u16 code triangle and the "
                    "adjacency bitsets in LDS; forest, dim-1 pass, dim-2 apparent walk); reduce = "
-                   "betti_wide_kernel_c16<6, true> (no LDS, 6 waves per SIMD: the reductions, statistics, outputs). "
+                   "betti_wide_kernel_c16<6, true> (no LDS, 8 waves per SIMD: the reductions, statistics, outputs). "
                    "FETCH_SIZE / WRITE_SIZE in KB (x1: the x2 gfx950 read correction is calibrated for streaming "
                    "reads); round 5's per-wave kernel: FETCH 83.2 MB x1 and WRITE 25.5 MB per complex, "
                    "profiles/r05_rc10_wide.json")}
