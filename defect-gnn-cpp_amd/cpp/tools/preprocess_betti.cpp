@@ -4,14 +4,17 @@
 // features of every structure, writes processed_path/betti/<id>.bin (save_betti_features format),
 // fits the PCA over all atoms and writes processed_path/pca_model.bin. Structures are sent to the
 // GPU in batches (one dgn_host_betti call per batch) instead of one OpenMP loop per structure.
-// --resume: a structure whose betti/<id>.bin already exists is loaded (load_betti_features) instead
-// of recomputed and its file is left untouched, as the Python upstream skips existing outputs
+// --resume: a structure whose betti/<id>.bin already exists (and matches its POSCAR's atom count) is
+// loaded (load_betti_features) instead of parsed and recomputed, and its file is left untouched, as the Python upstream skips existing outputs
 // (.reference_code/Defect_GNN/Betti_number.py:208-209); the PCA is still fitted over every atom.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <filesystem>
+#include <fstream>
 #include <map>
+#include <sstream>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
@@ -28,6 +31,22 @@ static std::pair<int, int> parse_structure_id(const std::string& id) {
     const size_t u = id.find('_');
     if (u == std::string::npos) return {std::stoi(id), 0};
     return {std::stoi(id.substr(0, u)), std::stoi(id.substr(u + 1))};
+}
+
+// atom count of a POSCAR from its header alone (line 7: the per-species counts, as io::parse_vasp
+// reads them): the --resume shape check of a saved betti/<id>.bin without parsing the coordinates
+static size_t vasp_atom_count(const std::string& path) {
+    std::ifstream f(path);
+    if (!f.is_open()) throw std::runtime_error("Could not open file: " + path);
+    std::string line;
+    for (int i = 0; i < 7; ++i)
+        if (!std::getline(f, line)) throw std::runtime_error("Truncated POSCAR: " + path);
+    std::stringstream ss(line);
+    size_t total = 0;
+    int c;
+    while (ss >> c) total += static_cast<size_t>(c);
+    if (total == 0) throw std::runtime_error("No atom counts in POSCAR: " + path);
+    return total;
 }
 
 static void log(const std::string& msg) { std::fprintf(stderr, "[preprocess_betti] %s\n", msg.c_str()); }
@@ -73,9 +92,9 @@ int main(int argc_in, char** argv_in) {
             std::vector<crystal::Structure> st;
             std::vector<size_t> todo;  // ids[i] to compute in this batch
             std::vector<dgn::MatrixXd> feats(hi - lo);
-            std::vector<crystal::Structure> parsed;
-            parsed.reserve(hi - lo);
-            for (size_t i = lo; i < hi; ++i) parsed.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
+            // --resume reads only the header of a structure whose betti/<id>.bin exists (shape check)
+            // and parses in full only the structures it computes: a raw file that no longer parses
+            // does not abort a batch whose features were saved
             for (size_t i = lo; i < hi; ++i) {
                 const std::string out = processed_path + "/betti/" + ids[i] + ".bin";
                 bool have = false;
@@ -84,8 +103,13 @@ int main(int argc_in, char** argv_in) {
                     // one of another shape (other structure) is recomputed, not trusted
                     try {
                         dgn::MatrixXd m = topology::load_betti_features(out);
-                        if (m.rows() == static_cast<std::ptrdiff_t>(parsed[i - lo].num_atoms()) &&
-                            m.cols() == topology::BETTI_FEATURE_DIM) {
+                        std::ptrdiff_t want = m.rows();
+                        try {
+                            want = static_cast<std::ptrdiff_t>(vasp_atom_count(raw_path + "/" + ids[i] + ".vasp"));
+                        } catch (const std::exception& e) {
+                            log(std::string("resume: ") + e.what() + "; keeping the saved " + out);
+                        }
+                        if (m.rows() == want && m.cols() == topology::BETTI_FEATURE_DIM) {
                             feats[i - lo] = std::move(m);
                             have = true;
                             ++skipped;
@@ -99,7 +123,7 @@ int main(int argc_in, char** argv_in) {
                 if (!have) todo.push_back(i);
             }
             st.reserve(todo.size());
-            for (size_t i : todo) st.push_back(parsed[i - lo]);
+            for (size_t i : todo) st.emplace_back(io::parse_vasp(raw_path + "/" + ids[i] + ".vasp"));
             std::vector<const crystal::Structure*> ptrs;
             for (const auto& s : st) ptrs.push_back(&s);
             if (!ptrs.empty()) {

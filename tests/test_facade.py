@@ -10,6 +10,7 @@ fixtures / the oracle; tools/preprocess_betti is run end to end.
 """
 import glob
 import os
+import shutil
 import subprocess
 
 import numpy as np
@@ -239,3 +240,29 @@ def test_preprocess_driver_resume_recomputes_bad_files(tmp_path, golden):
     for b, data in good.items():
         assert open(b, "rb").read() == data, b
     assert not glob.glob(str(outdir / "betti" / "*.tmp"))
+
+
+@pytest.mark.gpu
+def test_preprocess_driver_resume_skips_unparsable_raw(tmp_path, golden):
+    """--resume parses only what it computes: a raw POSCAR that no longer parses, whose
+    betti/<id>.bin was saved, does not abort the run (its features are reused), and the saved files
+    stay byte-identical."""
+    raw = tmp_path / "raw"
+    shutil.copytree(POSCARS, raw)
+    outdir = tmp_path / "processed"
+    exe = os.path.join(BIN, "preprocess_betti")
+    rc, _, err = _run([exe, str(raw), str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    good = {b: open(b, "rb").read() for b in glob.glob(str(outdir / "betti" / "*.bin"))}
+    pca1 = open(outdir / "pca_model.bin", "rb").read()
+    victim = raw / "741.vasp"
+    victim.write_text("".join(victim.read_text().splitlines(keepends=True)[:9]))  # header kept, coordinates cut
+    rc, _, err = _run([exe, "--resume", str(raw), str(outdir), "5", "6", "4"])
+    assert rc == 0, err
+    assert f"resume: {len(good)} existing" in err
+    for b, data in good.items():
+        assert open(b, "rb").read() == data, b
+    assert open(outdir / "pca_model.bin", "rb").read() == pca1
+    # without --resume the truncated file is parsed and the run fails loudly
+    rc, _, err = _run([exe, str(raw), str(tmp_path / "fresh"), "5", "6", "4"])
+    assert rc != 0 and "Truncated POSCAR" in err
