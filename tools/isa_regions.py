@@ -13,10 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.environ.get("ISA_CSRC") or os.path.join(ROOT, "defect-gnn-cpp_amd", "csrc")
 MARKS = [
     ("        for (int ci = 0; ci < nna; ++ci) {\n", "COL_TOP", True),
-    ("            int owner = find_pivot(npiv, tau);\n", "AFTER_FIND", True),
+    ("            int owner = (int)uni((uint32_t)find_pivot(npiv, tau));\n", "AFTER_FIND", True),
     ("            int v = 0;  // 0 = lazy: V == {this column}\n", "AFTER_APP", True),
-    ("                    tau = v > 0 ? pivot_of_V(dim, v, tau) : kInf;\n", "PIV", False),
-    ("                    tau = v > 0 ? pivot_of_V(dim, v, tau) : kInf;\n", "AFTER_PIV", True),
+    ("                    tau = uni64(v > 0 ? pivot_of_V(dim, v, tau) : kInf);\n", "PIV", False),
+    ("                    tau = uni64(v > 0 ? pivot_of_V(dim, v, tau) : kInf);\n", "AFTER_PIV", True),
     ("            // ---- tau is the pivot of this column ----\n", "FINAL", True),
     ("            npiv = (int)uni((uint32_t)(npiv + 1));\n            lds_sync();\n", "FINAL_END", True),
 ]
@@ -36,7 +36,7 @@ def main():
         s = s.replace(anchor, anchor + m if after else m + anchor, 1)
     open(p, "w").write(s)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-                    "-I" + out, "-I" + os.path.join(ROOT, "include"), "--save-temps", "-c", p, "-o",
+                    "-I" + out, "-I" + os.path.join(ROOT, "include"), "-mllvm", "-amdgpu-sched-strategy=iterative-minreg", "--save-temps", "-c", p, "-o",
                     os.path.join(out, "bk.o")], cwd=out, check=True, capture_output=True)
     asm = open(os.path.join(out, "betti_kernels-hip-amdgcn-amd-amdhsa-gfx950.s")).read().split("\n")
     np_ = os.environ.get("ISA_NP", "48")  # instantiation: 32, 44, 48 or 64
