@@ -464,9 +464,16 @@ struct Complex {
             sel = (uint32_t)k > va ? 0x04020100u : ((uint32_t)k > vb ? 0x02040100u : ((uint32_t)k > vcc_ ? 0x02010400u : 0x02010004u));
         }
         const uint32_t nk = __builtin_amdgcn_perm(kc, ~vsp, sel);
-        return ((uint64_t)dd << 32) | (uint64_t)nk;
+        return __builtin_bit_cast(uint64_t, make_uint2(nk, dd));  // (dd, nk) as one register pair
     }
 
+    // key - base as one v_lshl_add_u64 on the (nk, dd) register pair (the compiler's own form adds
+    // the two halves separately: three VALU per V entry)
+    __device__ static uint64_t rel_key(uint64_t key, uint64_t nbase) {
+        uint64_t r;
+        asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(r) : "v"(key), "s"(nbase));
+        return r;
+    }
     // Pivot of the column sum(delta s, s in V) (whole wave): the F-minimal cofacet of odd
     // multiplicity, restricted to keys above `floor` (the column's previous pivot: adding the
     // owner column cancels it and every other entry of both columns is larger). Lane k
@@ -485,6 +492,7 @@ struct Complex {
             // above every key > floor, so one unsigned minimum skips them (floor is a real key,
             // never kInf)
             const uint64_t base = floor + 1;
+            const uint64_t nbase = 0ull - base;
             uint64_t lmin = kInf;
             // kPvUnroll V entries per step, their distance reads in flight together, then the rest;
             // entries 0..63 (register set 0) and 64.. (set 1) in separate loops, so no entry pays a
@@ -495,12 +503,12 @@ struct Complex {
                 for (; i + kPvUnroll <= cnt; i += kPvUnroll) {
                     uint64_t kq[kPvUnroll];
 #pragma unroll
-                    for (int u = 0; u < kPvUnroll; ++u) kq[u] = cofacet_key(dim, k, kc, rl(vs, i + u), rl(vdb, i + u)) - base;
+                    for (int u = 0; u < kPvUnroll; ++u) kq[u] = rel_key(cofacet_key(dim, k, kc, rl(vs, i + u), rl(vdb, i + u)), nbase);
 #pragma unroll
                     for (int u = 0; u < kPvUnroll; ++u) lmin = kq[u] < lmin ? kq[u] : lmin;
                 }
                 for (; i < cnt; ++i) {
-                    const uint64_t key = cofacet_key(dim, k, kc, rl(vs, i), rl(vdb, i)) - base;
+                    const uint64_t key = rel_key(cofacet_key(dim, k, kc, rl(vs, i), rl(vdb, i)), nbase);
                     lmin = key < lmin ? key : lmin;
                 }
             };
