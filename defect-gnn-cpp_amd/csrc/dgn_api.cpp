@@ -593,7 +593,9 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                     int64_t slice = std::max<int64_t>(
                         1, std::min<int64_t>({nwide, (int64_t(16) << 30) / (20 * rstride), INT32_MAX / rstride}));
                     // The walk pass's per-complex outputs (matrix, lists: ~1.7 MB at 340 points), two
-                    // slices' worth within a quarter of the HBM that is free or already theirs, <= 32 GB.
+                    // slices' worth within half of the HBM that is free or already theirs, <= 32 GB
+                    // (a quarter cut the slices below the reductions' 8,192 resident waves in a process
+                    // holding ~40 GB elsewhere, the bench's config-4 shard: 7-9 % slower at 10 A).
                     // Slice q's walk pass (LDS- and issue-bound, one workgroup per CU) runs on the context
                     // stream while slice q - 1's reductions (LDS-free, latency-bound) run on a second
                     // stream: double-buffered codes and walk outputs, ordered by events
@@ -603,7 +605,7 @@ int betti_impl(dgn_ctx* c, const dgn_batch* b, double rc, double* features, int3
                         size_t free_b = 0, total_b = 0;
                         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
                         const int64_t wbudget = std::min<int64_t>(
-                            int64_t(32) << 30, std::max<int64_t>(int64_t(1) << 30, ((int64_t)free_b + (int64_t)c->b_walk.bytes) / 4));
+                            int64_t(32) << 30, std::max<int64_t>(int64_t(1) << 30, ((int64_t)free_b + (int64_t)c->b_walk.bytes) / 2));
                         slice = std::max<int64_t>(1, std::min<int64_t>(slice, wbudget / (nbuf * walk_bytes)));
                     }
                     // equal slices: a short last slice leaves its launch's resident waves idle behind

@@ -15,6 +15,18 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 dev = torch.device("cuda:0")
 ctx = dgn.Context(0)
+if os.environ.get("DGN_WIDE_CAP"):  # A/B knob for this tool only
+    ctx.set_debug(abi.DEBUG_WIDE_CAP, int(os.environ["DGN_WIDE_CAP"]))
+if os.environ.get("PRE_HEADLINE"):  # the bench's config-4 shard (graph + Betti at rc 5) first, kept alive
+    head = Shard(dgn, abi, "fcc", 4, 8192, 0, dev)
+    gp = abi.graph_params(r_cutoff=5.0, max_neighbors=20, rbf_cutoff=5.0, rbf_dr=0.1, rbf_dtype=dgn.DGN_F64)
+    head.alloc_graph(ctx, gp, abi.lib().dgn_rbf_bins(5.0, 0.1), torch.float64)
+    head.alloc_betti()
+    for _ in range(3):
+        head.step(ctx, gp, 5.0)
+    torch.cuda.synchronize(dev)
+    f, t = torch.cuda.mem_get_info(dev)
+    print(f"headline shard done; free {f / 2**30:.1f} of {t / 2**30:.1f} GiB", flush=True)
 if os.environ.get("PRE_B"):  # a smaller batch through the same context first (bench.py's side-line order)
     pre = Shard(dgn, abi, "fcc", 4, int(os.environ["PRE_B"]), 0, dev)
     pre.alloc_betti()
